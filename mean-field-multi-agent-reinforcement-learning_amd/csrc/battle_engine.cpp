@@ -1,0 +1,642 @@
+// battle_engine.cpp -- host runtime of the Battle engine + its C ABI.
+//
+// The C ABI is the reference's own (runtime_api.h:118-181: env_* / gridworld_*), so the
+// reference python wrapper (gridworld.py, via ctypes) and this repository's drop-in
+// `magent` package both bind it unchanged.  Those calls work on env 0 and move data
+// through host buffers.  The batched device API (mfx_battle_*) drives all E envs of an
+// engine with device pointers and never leaves HBM.  See include/magent_amd.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "battle_kernels.h"
+#include "battle_layout.h"
+#include "mfx_common.h"
+
+namespace mfx {
+
+// ------------------------------------------------------------------ host-side ranges
+struct HostRange {                                  // Range.h:14-113
+    int w = 0, h = 0, count = 0, x1 = 0, y1 = 0, x2 = 0, y2 = 0;
+    std::vector<uint8_t> in;
+    std::vector<int> dx, dy;
+};
+
+static HostRange circle_range(float radius, float inner, int parity) {   // Range.h:171-215
+    const double eps = 1e-8;
+    HostRange r;
+    int width = 2 * (int)(radius + eps) + parity;
+    const int center = (int)radius;
+    if (width % 2 != parity) width++;
+    r.w = r.h = width;
+    r.in.assign((size_t)width * width, 0);
+    const double delta = parity == 0 ? 0.5 : 0;
+    for (int i = 0; i < width; i++)
+        for (int j = 0; j < width; j++) {
+            const double ddx = std::fabs(j - center + delta), ddy = std::fabs(i - center + delta);
+            const double dis = std::sqrt(ddx * ddx + ddy * ddy);
+            if (dis < radius + eps && dis > inner - eps) {
+                r.in[(size_t)i * width + j] = 1;
+                r.dx.push_back(j - center);
+                r.dy.push_back(i - center);
+            }
+        }
+    r.count = (int)r.dx.size();
+    r.x1 = r.y1 = -center;
+    r.x2 = r.y2 = width - center - 1;
+    return r;
+}
+
+static HostRange sector_range(float angle, float radius, int parity) {   // Range.h:121-166
+    const double PI = 3.1415926536, eps = 0.00001;
+    HostRange r;
+    const int height = (int)(radius + 0.5);
+    int width = (int)(2 * radius * std::sin(angle / 2 * (PI / 180)) + 0.5);
+    if (width % 2 != parity) width--;
+    r.w = width; r.h = height;
+    r.in.assign((size_t)std::max(0, width * height), 0);
+    for (int i = 0; i < height; i++)
+        for (int j = 0; j < width; j++) {
+            const double ddx = std::fabs(j - (width - 1) / 2.0), ddy = std::fabs((double)(height - i));
+            const double dis = std::sqrt(ddx * ddx + ddy * ddy);
+            if (dis < radius + 0.2 + eps && ddx / ddy < std::tan(angle / 2 * PI / 180) + eps) {
+                r.in[(size_t)i * width + j] = 1;
+                r.dx.push_back(j - width / 2);
+                r.dy.push_back(i - height);
+            }
+        }
+    r.count = (int)r.dx.size();
+    r.x1 = -width / 2; r.y1 = -height; r.x2 = (width - 1) / 2; r.y2 = -1;
+    return r;
+}
+
+struct AgentTypeSpec {                               // AgentType.cc:28-131
+    std::string name;
+    int width = 1, length = 1;
+    float speed = 1, hp = 1, view_radius = 1, view_angle = 360, attack_radius = 0, attack_angle = 0;
+    float hear_radius = 0, speak_radius = 0;
+    int speak_ability = 0;
+    float damage = 0, trace = 0, eat_ability = 0, step_recover = 0, kill_supply = 0, food_supply = 0;
+    bool attack_in_group = false, can_absorb = false;
+    float step_reward = 0, kill_reward = 0, dead_penalty = 0, attack_penalty = 0;
+    HostRange view, attack, move;
+    int turn_base = 0, attack_base = 0, n_action = 0;
+};
+
+// ------------------------------------------------------------------ the engine
+class BattleEngine {
+public:
+    // --- configuration (GridWorld.cc:126-155)
+    int W = 0, H = 0, emb = 0;
+    bool minimap = false, food = false, turn = false, goal = false;
+    bool large_map = false; int n_sep = 8;
+    uint32_t rng_init = 1;                          // seed(0) -> state 1 (GridWorld.cc:31)
+    std::map<std::string, AgentTypeSpec> types;
+    std::vector<std::string> group_types;
+    struct Sym { int group, index; };
+    struct Node { int op; std::vector<int> raw; };
+    struct Rule { int on; std::vector<int> recv; std::vector<float> val; bool terminal; };
+    std::vector<Sym> syms; std::vector<Node> nodes; std::vector<Rule> rules;
+
+    // --- device
+    int E = 1;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    GameParams gp{};
+    GameParams* d_gp = nullptr;
+    State s{};
+    uint32_t* d_sort = nullptr;
+    int32_t* d_err = nullptr;
+    bool allocated = false;
+    int max_ids = 0;                                 // upper bound of id_counter over envs
+    std::vector<int> group_ub;                       // upper bound of grp_n per group
+    int pending_ub = 0;                              // upper bound of queued actions
+    // drop-in staging (env 0, host buffers)
+    DevBuf<float> st_view, st_feat, st_f32;
+    DevBuf<int> st_i32, st_xs, st_ys;
+    DevBuf<uint8_t> st_u8;
+
+    ~BattleEngine() { release(); if (own_stream && stream) (void)hipStreamDestroy(stream); }
+
+    void release() {
+        for (void* p : {(void*)s.cells, (void*)s.xy, (void*)s.hp, (void*)s.next_r, (void*)s.last_r,
+                        (void*)s.last_act, (void*)s.op_obj, (void*)s.meta, (void*)s.grp_ids, (void*)s.grp_n,
+                        (void*)s.grp_dead, (void*)s.grp_reward, (void*)s.id_counter, (void*)s.rng, (void*)s.atk,
+                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)d_sort, (void*)d_gp,
+                        (void*)d_err})
+            if (p) (void)hipFree(p);
+        s = State{}; d_sort = nullptr; d_gp = nullptr; d_err = nullptr; allocated = false;
+    }
+
+    int n_groups() const { return (int)group_types.size(); }
+    AgentTypeSpec& gtype(int g) { return types.at(group_types.at(g)); }
+    int group2channel(int g) const { return (food ? 2 : 1) + g * (minimap ? 3 : 2); }
+    int feature_size(int g) {
+        int f = emb + gtype(g).n_action + 1;
+        if (goal) f += 2;
+        if (minimap) f += 2;
+        return f;
+    }
+
+    // ------------------------------------------------------------------ config
+    int set_config(const char* key, void* p) {
+        if (!strcmp(key, "map_width")) W = *(int*)p;
+        else if (!strcmp(key, "map_height")) H = *(int*)p;
+        else if (!strcmp(key, "food_mode")) food = *(bool*)p;
+        else if (!strcmp(key, "turn_mode")) turn = *(bool*)p;
+        else if (!strcmp(key, "minimap_mode")) minimap = *(bool*)p;
+        else if (!strcmp(key, "goal_mode")) goal = *(bool*)p;
+        else if (!strcmp(key, "embedding_size")) emb = *(int*)p;
+        else if (!strcmp(key, "render_dir")) { /* rendering is out of scope */ }
+        else if (!strcmp(key, "seed")) {
+            const unsigned long sv = (unsigned long)(long)*(int*)p;
+            const uint64_t x = sv % 2147483647UL;
+            rng_init = x ? (uint32_t)x : 1u;
+            if (allocated) {
+                std::vector<uint32_t> h((size_t)E, rng_init);
+                MFX_HIP(hipMemcpyAsync(s.rng, h.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice, stream));
+                MFX_HIP(hipStreamSynchronize(stream));
+            }
+        } else return fail("invalid argument in set_config: %s", key);
+        if (food || turn || goal) return fail("food_mode/turn_mode/goal_mode are not supported (DESIGN.md scope)");
+        return 0;
+    }
+
+    int register_type(const char* name, int n, const char** keys, const float* values) {
+        if (types.count(name)) return fail("duplicated name of agent type: %s", name);
+        AgentTypeSpec t;
+        t.name = name;
+        for (int i = 0; i < n; i++) {
+            const char* k = keys[i];
+            const float v = values[i];
+#define MFX_I(f) if (!strcmp(k, #f)) { t.f = (int)(v + 0.5); continue; }
+#define MFX_F(f) if (!strcmp(k, #f)) { t.f = v; continue; }
+#define MFX_B(f) if (!strcmp(k, #f)) { t.f = (bool)(int)(v + 0.5); continue; }
+            MFX_I(width) MFX_I(length) MFX_F(speed) MFX_F(hp) MFX_F(view_radius) MFX_F(view_angle)
+            MFX_F(attack_radius) MFX_F(attack_angle) MFX_F(hear_radius) MFX_F(speak_radius)
+            MFX_I(speak_ability) MFX_F(damage) MFX_F(trace) MFX_F(eat_ability) MFX_F(step_recover)
+            MFX_F(kill_supply) MFX_F(food_supply) MFX_B(attack_in_group) MFX_B(can_absorb)
+            MFX_F(step_reward) MFX_F(kill_reward) MFX_F(dead_penalty) MFX_F(attack_penalty)
+#undef MFX_I
+#undef MFX_F
+#undef MFX_B
+            // accepted and then recomputed from the body size (AgentType.cc:117-120)
+            if (!strcmp(k, "view_x_offset") || !strcmp(k, "view_y_offset") || !strcmp(k, "att_x_offset") ||
+                !strcmp(k, "att_y_offset") || !strcmp(k, "turn_x_offset") || !strcmp(k, "turn_y_offset"))
+                continue;
+            return fail("invalid agent config in register_agent_type: %s", k);
+        }
+        if (t.width != 1 || t.length != 1) return fail("only 1x1 agent bodies are supported");
+        if (t.can_absorb) return fail("can_absorb is not supported");
+        const int parity = t.width % 2;
+        if (t.view_angle >= 180) {
+            if (std::fabs(t.view_angle - 360) > 1e-5) return fail("only angle = 360 when angle > 180");
+            t.view = circle_range(t.view_radius, 0, parity);
+        } else t.view = sector_range(t.view_angle, t.view_radius, parity);
+        if (t.attack_angle >= 180) {
+            if (std::fabs(t.attack_angle - 360) > 1e-5) return fail("only angle = 360 when angle > 180");
+            t.attack = circle_range(t.attack_radius, t.width / 2.0f, parity);
+        } else t.attack = sector_range(t.attack_angle, t.attack_radius, parity);
+        t.move = circle_range(t.speed, 0, 1);
+        t.turn_base = t.move.count;
+        t.attack_base = t.turn_base;
+        t.n_action = t.attack_base + t.attack.count;
+        if (t.view.w * t.view.h > kMaxViewCells || t.view.w <= 0 || t.view.h <= 0)
+            return fail("view range too large (max %d cells)", kMaxViewCells);
+        if (t.move.count > kMaxRangeCount || t.attack.count > kMaxRangeCount)
+            return fail("move/attack range too large (max %d cells)", kMaxRangeCount);
+        types.emplace(t.name, std::move(t));
+        return 0;
+    }
+
+    int new_group(const char* type_name, int* group) {
+        if (!types.count(type_name)) return fail("invalid name of agent type in new_group: %s", type_name);
+        if (n_groups() >= kMaxGroups) return fail("at most %d groups", kMaxGroups);
+        if (allocated) return fail("new_group after the first reset is not supported");
+        *group = n_groups();
+        group_types.push_back(type_name);
+        return 0;
+    }
+
+    // ------------------------------------------------------------------ compile
+    int build_params() {
+        const int G = n_groups();
+        if (W <= 0 || H <= 0) return fail("map_width/map_height not set");
+        if (W > 0xFFFF || H > 0xFFFF) return fail("map too large");
+        if (G == 0) return fail("no groups");
+        GameParams p{};
+        p.W = W; p.H = H; p.n_groups = G; p.minimap = minimap; p.emb = emb;
+        p.n_ch = group2channel(G);
+        if ((long)W * H > 99 * 99) { large_map = true; n_sep = (long)W * H > 1000 * 1000 ? 16 : 8; }  // sticky
+        p.large_map = large_map; p.n_sep = n_sep; p.band_w = (W + n_sep - 1) / n_sep;
+        for (int g = 0; g < G; g++) {
+            AgentTypeSpec& t = gtype(g);
+            TypeParams& T = p.type[g];
+            T.hp = t.hp; T.damage = t.damage; T.step_recover = t.step_recover; T.kill_supply = t.kill_supply;
+            T.step_reward = t.step_reward; T.kill_reward = t.kill_reward; T.dead_penalty = t.dead_penalty;
+            T.attack_penalty = t.attack_penalty; T.attack_in_group = t.attack_in_group;
+            T.n_action = t.n_action; T.turn_base = t.turn_base; T.attack_base = t.attack_base;
+            T.n_move = t.move.count; T.n_attack = t.attack.count;
+            T.view_w = t.view.w; T.view_h = t.view.h;
+            T.view_x1 = t.width / 2 + t.view.x1;     // eye = pos + view offset (Map.cc:146-149)
+            T.view_y1 = t.length / 2 + t.view.y1;
+            T.att_x_off = t.width / 2; T.att_y_off = t.length / 2;
+            for (int i = 0; i < t.move.count; i++) { T.move_dx[i] = (int8_t)t.move.dx[i]; T.move_dy[i] = (int8_t)t.move.dy[i]; }
+            for (int i = 0; i < t.attack.count; i++) { T.att_dx[i] = (int8_t)t.attack.dx[i]; T.att_dy[i] = (int8_t)t.attack.dy[i]; }
+            for (int i = 0; i < t.view.w * t.view.h; i++) T.view_mask[i] = t.view.in[i];
+            p.feat_size[g] = feature_size(g);
+            if (t.view.w != gtype(0).view.w || t.view.h != gtype(0).view.h)
+                return fail("all groups must share one view size");
+        }
+        // reward rules: one binary event (attack/kill/collide) between two 'any' symbols of
+        // different groups, receivers = the event's subject and/or object.
+        if ((int)rules.size() > kMaxRules) return fail("at most %d reward rules", kMaxRules);
+        p.n_rules = (int)rules.size();
+        for (size_t r = 0; r < rules.size(); r++) {
+            const Rule& R = rules[r];
+            if (R.on < 0 || R.on >= (int)nodes.size()) return fail("reward rule %zu: bad event node", r);
+            const Node& N = nodes[R.on];
+            int op;
+            if (N.op == kEvAttack) op = kOpAttack;
+            else if (N.op == kEvKill) op = kOpKill;
+            else if (N.op == kEvCollide) op = kOpCollide;
+            else return fail("reward rule %zu: only attack/kill/collide events are supported", r);
+            if (N.raw.size() < 2) return fail("reward rule %zu: malformed event", r);
+            const int sa = N.raw[0], sb = N.raw[1];
+            if (sa >= (int)syms.size() || sb >= (int)syms.size()) return fail("reward rule %zu: bad symbol", r);
+            if (syms[sa].index != -1 || syms[sb].index != -1 || syms[sa].group == syms[sb].group)
+                return fail("reward rule %zu: symbols must be 'any' agents of two different groups", r);
+            if ((int)R.recv.size() > kMaxRecv) return fail("reward rule %zu: too many receivers", r);
+            RuleParams& RP = p.rules[r];
+            RP.op = op; RP.subj_group = syms[sa].group; RP.obj_group = syms[sb].group;
+            RP.n_recv = (int)R.recv.size(); RP.terminal = R.terminal;
+            for (size_t k = 0; k < R.recv.size(); k++) {
+                if (R.recv[k] != sa && R.recv[k] != sb)
+                    return fail("reward rule %zu: receivers must be the event's subject or object", r);
+                RP.recv_is_obj[k] = R.recv[k] == sb;
+                RP.val[k] = R.val[k];
+            }
+        }
+        gp = p;
+        return 0;
+    }
+
+    template <class T> static void alloc(T*& ptr, size_t n) {
+        MFX_HIP_THROW(hipMalloc(&ptr, sizeof(T) * std::max<size_t>(n, 1)));
+    }
+
+    // (Re)allocate per-agent arrays with a new capacity, preserving contents row by row.
+    template <class T> void grow(T*& ptr, size_t rows, size_t old_cap, size_t new_cap) {
+        T* np;
+        alloc(np, rows * new_cap);
+        if (ptr && old_cap)
+            MFX_HIP_THROW(hipMemcpy2DAsync(np, new_cap * sizeof(T), ptr, old_cap * sizeof(T), old_cap * sizeof(T),
+                                           rows, hipMemcpyDeviceToDevice, stream));
+        MFX_HIP_THROW(hipStreamSynchronize(stream));
+        if (ptr) (void)hipFree(ptr);
+        ptr = np;
+    }
+
+    void ensure_capacity(int need_ids, int need_actions) {
+        const int G = n_groups();
+        if (need_ids > s.cap) {
+            int nc = std::max(64, s.cap);
+            while (nc < need_ids) nc *= 2;
+            if (nc > 0xFFFE) nc = 0xFFFE;
+            const int oc = s.cap;
+            grow(s.xy, E, oc, nc); grow(s.hp, E, oc, nc); grow(s.next_r, E, oc, nc); grow(s.last_r, E, oc, nc);
+            grow(s.last_act, E, oc, nc); grow(s.op_obj, E, oc, nc); grow(s.meta, E, oc, nc);
+            grow(s.grp_ids, (size_t)E * G, oc, nc);
+            s.cap = nc;
+        }
+        if (need_actions > s.acap) {
+            int na = std::max(128, s.acap);
+            while (na < need_actions) na *= 2;
+            const int oa = s.acap;
+            grow(s.atk, E, oa, na); grow(s.mov, E, oa, na); grow(d_sort, E, oa, na);
+            s.acap = na;
+        }
+    }
+
+    int reset() {
+        MFX_CHECK(build_params());
+        try {
+            const int G = n_groups();
+            if (!allocated) {
+                MFX_HIP_THROW(hipGetDevice(&device));
+                if (!stream) { MFX_HIP_THROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); own_stream = true; }
+                s.E = E;
+                s.cells_n = W * H;
+                alloc(s.cells, (size_t)E * W * H);
+                alloc(s.grp_n, (size_t)E * G); alloc(s.grp_dead, (size_t)E * G); alloc(s.grp_reward, (size_t)E * G);
+                alloc(s.id_counter, E); alloc(s.rng, E); alloc(s.n_atk, E); alloc(s.n_mov, E); alloc(s.done, E);
+                alloc(d_gp, 1); alloc(d_err, 1);
+                MFX_HIP_THROW(hipMemset(d_err, 0, sizeof(int32_t)));
+                s.err = d_err;
+                std::vector<uint32_t> h((size_t)E, rng_init);
+                MFX_HIP_THROW(hipMemcpy(s.rng, h.data(), sizeof(uint32_t) * E, hipMemcpyHostToDevice));
+                group_ub.assign(G, 0);
+                allocated = true;
+                ensure_capacity(64, 128);
+            } else if (s.cells_n != W * H) {
+                return fail("map size changed after the first reset");
+            }
+            MFX_HIP_THROW(hipMemcpyAsync(d_gp, &gp, sizeof(GameParams), hipMemcpyHostToDevice, stream));
+            MFX_HIP_THROW(launch_reset(d_gp, s, stream));
+            max_ids = 0;
+            std::fill(group_ub.begin(), group_ub.end(), 0);
+            pending_ub = 0;
+            return 0;
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+    }
+
+    // same placement for every env (host arrays)
+    int add_agents(int group, int n, const char* method, const int* xs, const int* ys) {
+        if (!allocated) return fail("add_agents before reset");
+        if (group >= n_groups() || group < -1) return fail("invalid group handle in add_agents: %d", group);
+        int m, count;
+        std::vector<int> hx, hy;
+        if (!strcmp(method, "custom")) {
+            m = 0; count = n;
+            hx.assign(xs, xs + n); hy.assign(ys, ys + n);
+        } else if (!strcmp(method, "random")) {
+            m = 1; count = n;
+        } else if (!strcmp(method, "fill")) {
+            m = 2; count = std::max(0, xs[2]) * std::max(0, xs[3]);
+            hx.assign(xs, xs + 4);
+        } else return fail("unsupported method in add_agents: %s", method);
+        try {
+            if (group >= 0) {
+                ensure_capacity(max_ids + count, 0);
+                max_ids += count;
+                group_ub[group] += count;
+            }
+            if (hx.empty()) hx.push_back(0);
+            if (hy.empty()) hy.push_back(0);
+            st_xs.ensure(hx.size()); st_ys.ensure(hy.size());
+            MFX_HIP_THROW(hipMemcpyAsync(st_xs.p, hx.data(), sizeof(int) * hx.size(), hipMemcpyHostToDevice, stream));
+            MFX_HIP_THROW(hipMemcpyAsync(st_ys.p, hy.data(), sizeof(int) * hy.size(), hipMemcpyHostToDevice, stream));
+            MFX_HIP_THROW(launch_add_agents(d_gp, s, group, n, m, st_xs.p, st_ys.p, 0, stream));
+            MFX_HIP_THROW(hipStreamSynchronize(stream));   // host vectors go out of scope
+            return check_err();
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+    }
+
+    int check_err() {
+        int32_t h = 0;
+        MFX_HIP(hipMemcpyAsync(&h, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        if (h) {
+            MFX_HIP(hipMemsetAsync(d_err, 0, sizeof(int32_t), stream));
+            static const char* msg[] = {"", "", "agent capacity exceeded", "no blank position for random placement",
+                                        "output row capacity smaller than the group", "invalid action id",
+                                        "action buffer overflow"};
+            return fail("device error %d: %s", h, h > 0 && h < 7 ? msg[h] : "unknown");
+        }
+        return 0;
+    }
+
+    int num_env0(int g) {
+        int32_t n = 0;
+        MFX_HIP(hipMemcpyAsync(&n, s.grp_n + g, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        return n;
+    }
+
+    // ------------------------------------------------------------------ batched device API
+    int observe(int g, float* d_view, float* d_feat, int rowcap) {
+        if (!allocated || g < 0 || g >= n_groups()) return fail("observe: bad state or group");
+        MFX_HIP(launch_observe(gp, d_gp, s, g, group_ub[g], d_view, d_feat, rowcap, stream));
+        return 0;
+    }
+    int set_action(int g, const int* d_actions, int rowcap) {
+        if (!allocated || g < 0 || g >= n_groups()) return fail("set_action: bad state or group");
+        pending_ub += group_ub[g];
+        try { ensure_capacity(0, pending_ub); } catch (const HipFailure& f) { return fail("%s", f.what()); }
+        MFX_HIP(launch_set_action(d_gp, s, g, d_actions, rowcap, stream));
+        return 0;
+    }
+    int step(int* d_done) {
+        if (!allocated) return fail("step before reset");
+        MFX_HIP(launch_step(gp, d_gp, s, max_ids, d_sort, stream));
+        pending_ub = 0;
+        if (d_done) MFX_HIP(hipMemcpyAsync(d_done, s.done, sizeof(int32_t) * E, hipMemcpyDeviceToDevice, stream));
+        return 0;
+    }
+    int get(int g, int what, void* d_out, int rowcap) {
+        if (!allocated || g < 0 || g >= n_groups()) return fail("get: bad state or group");
+        MFX_HIP(launch_get(d_gp, s, g, what, d_out, rowcap, stream));
+        return 0;
+    }
+    int clear_dead() {
+        if (!allocated) return fail("clear_dead before reset");
+        MFX_HIP(launch_clear_dead(d_gp, s, stream));
+        return 0;
+    }
+
+    // ------------------------------------------------------------------ drop-in (env 0, host buffers)
+    int host_observe(int g, float** bufs) {
+        if (!allocated) return fail("get_observation before reset");
+        const int n = num_env0(g);
+        if (n == 0) return 0;
+        const TypeParams& T = gp.type[g];
+        const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
+        const int rowcap = std::max(group_ub[g], 4);
+        st_view.ensure((size_t)E * rowcap * VF);
+        st_feat.ensure((size_t)E * rowcap * F);
+        MFX_CHECK(observe(g, st_view.p, st_feat.p, rowcap));
+        MFX_HIP(hipMemcpyAsync(bufs[0], st_view.p, sizeof(float) * n * VF, hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipMemcpyAsync(bufs[1], st_feat.p, sizeof(float) * n * F, hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        return check_err();
+    }
+    int host_set_action(int g, const int* actions) {
+        if (!allocated) return fail("set_action before reset");
+        const int n = num_env0(g);
+        const int rowcap = std::max(group_ub[g], 1);
+        st_i32.ensure((size_t)E * rowcap);
+        if (n) MFX_HIP(hipMemcpyAsync(st_i32.p, actions, sizeof(int) * n, hipMemcpyHostToDevice, stream));
+        MFX_CHECK(set_action(g, st_i32.p, rowcap));
+        MFX_HIP(hipStreamSynchronize(stream));
+        return check_err();
+    }
+    int host_step(int* done) {
+        MFX_CHECK(step(nullptr));
+        int32_t d = 0;
+        MFX_HIP(hipMemcpyAsync(&d, s.done, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        *done = d;
+        return check_err();
+    }
+    int host_get(int g, int what, void* out, size_t elem_bytes) {
+        const int n = num_env0(g);
+        if (n == 0) return 0;
+        const int rowcap = std::max(group_ub[g], 1);
+        st_u8.ensure((size_t)E * rowcap * elem_bytes);
+        MFX_CHECK(get(g, what, st_u8.p, rowcap));
+        MFX_HIP(hipMemcpyAsync(out, st_u8.p, elem_bytes * n, hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        return check_err();
+    }
+
+    int get_info(int group, const char* name, void* buf) {   // GridWorld.cc:777-978
+        int* ib = (int*)buf;
+        const int G = n_groups();
+        const bool need_group = strcmp(name, "both_attack") != 0;
+        if (need_group && (group < 0 || group >= G)) return fail("invalid group %d for get_info(%s)", group, name);
+        if (!strcmp(name, "num")) { if (!allocated) { ib[0] = 0; return 0; } ib[0] = num_env0(group); return 0; }
+        if (!strcmp(name, "id")) return host_get(group, kGetId, buf, 4);
+        if (!strcmp(name, "pos")) return host_get(group, kGetPos, buf, 8);
+        if (!strcmp(name, "alive")) return host_get(group, kGetAlive, buf, 1);
+        AgentTypeSpec& t = gtype(group);
+        if (!strcmp(name, "action_space")) { ib[0] = t.n_action; return 0; }
+        if (!strcmp(name, "view_space")) { ib[0] = t.view.h; ib[1] = t.view.w; ib[2] = group2channel(G); return 0; }
+        if (!strcmp(name, "feature_space")) { ib[0] = feature_size(group); return 0; }
+        if (!strcmp(name, "attack_base")) { ib[0] = t.attack_base; return 0; }
+        if (!strcmp(name, "view2attack")) {
+            for (int i = 0; i < t.view.w * t.view.h; i++) ib[i] = -1;
+            for (int i = 0; i < t.attack.count; i++)
+                ib[(t.attack.dy[i] - t.view.y1) * t.view.w + (t.attack.dx[i] - t.view.x1)] = i;
+            return 0;
+        }
+        if (!strcmp(name, "both_attack")) { ib[0] = 0; return 0; }   // statistics are compiled off (GridWorld.cc:501)
+        return fail("unsupported info name in get_info: %s", name);
+    }
+};
+
+}  // namespace mfx
+
+using mfx::BattleEngine;
+
+// ============================================================================ C ABI
+#define MFX_ENV(h) static_cast<BattleEngine*>(h)
+#define MFX_GUARD(expr)                                                          \
+    try {                                                                        \
+        return (expr);                                                           \
+    } catch (const std::exception& ex) {                                         \
+        return mfx::fail("%s", ex.what());                                       \
+    }
+
+extern "C" {
+
+// ---- reference runtime_api.h:118-181 ------------------------------------------------
+MFX_API int env_new_game(void** game, const char* name) {
+    if (strcmp(name, "GridWorld") != 0) return mfx::fail("invalid name of game: %s", name);
+    MFX_GUARD((*game = new BattleEngine(), 0));
+}
+MFX_API int env_delete_game(void* game) { delete MFX_ENV(game); return 0; }
+MFX_API int env_config_game(void* game, const char* name, void* value) { MFX_GUARD(MFX_ENV(game)->set_config(name, value)); }
+MFX_API int env_reset(void* game) { MFX_GUARD(MFX_ENV(game)->reset()); }
+MFX_API int env_get_observation(void* game, int group, float** buffer) { MFX_GUARD(MFX_ENV(game)->host_observe(group, buffer)); }
+MFX_API int env_set_action(void* game, int group, const int* actions) { MFX_GUARD(MFX_ENV(game)->host_set_action(group, actions)); }
+MFX_API int env_step(void* game, int* done) { MFX_GUARD(MFX_ENV(game)->host_step(done)); }
+MFX_API int env_get_reward(void* game, int group, float* buffer) {
+    MFX_GUARD(MFX_ENV(game)->host_get(group, mfx::kGetReward, buffer, 4));
+}
+MFX_API int env_get_info(void* game, int group, const char* name, void* buffer) {
+    MFX_GUARD(MFX_ENV(game)->get_info(group, name, buffer));
+}
+MFX_API int env_render(void* game) { (void)game; return 0; }              // visualization: out of scope
+MFX_API int env_render_next_file(void* game) { (void)game; return 0; }
+
+MFX_API int gridworld_register_agent_type(void* game, const char* name, int n, const char** keys, float* values) {
+    MFX_GUARD(MFX_ENV(game)->register_type(name, n, keys, values));
+}
+MFX_API int gridworld_new_group(void* game, const char* agent_type_name, int* group) {
+    MFX_GUARD(MFX_ENV(game)->new_group(agent_type_name, group));
+}
+MFX_API int gridworld_add_agents(void* game, int group, int n, const char* method, const int* pos_x, const int* pos_y,
+                                 const int* dir) {
+    (void)dir;   // turn_mode is off: every agent faces NORTH (GridWorld.cc:264)
+    MFX_GUARD(MFX_ENV(game)->add_agents(group, n, method, pos_x, pos_y));
+}
+MFX_API int gridworld_clear_dead(void* game) {
+    BattleEngine* e = MFX_ENV(game);
+    MFX_GUARD(e->clear_dead() ? -1 : (hipStreamSynchronize(e->stream) == hipSuccess ? 0 : -1));
+}
+MFX_API int gridworld_set_goal(void* game, int group, const char* method, const int* linear_buffer) {
+    (void)game; (void)group; (void)method; (void)linear_buffer;
+    return mfx::fail("set_goal is deprecated in the reference and not supported");
+}
+MFX_API int gridworld_define_agent_symbol(void* game, int no, int group, int index) {
+    BattleEngine* e = MFX_ENV(game);
+    if (no < 0) return mfx::fail("bad symbol number");
+    if ((size_t)no >= e->syms.size()) e->syms.resize(no + 1);
+    e->syms[no] = {group, index};
+    return 0;
+}
+MFX_API int gridworld_define_event_node(void* game, int no, int op, int* inputs, int n_inputs) {
+    BattleEngine* e = MFX_ENV(game);
+    if (no < 0) return mfx::fail("bad event node number");
+    if ((size_t)no >= e->nodes.size()) e->nodes.resize(no + 1);
+    e->nodes[no].op = op;
+    e->nodes[no].raw.assign(inputs, inputs + n_inputs);
+    return 0;
+}
+// The reference python passes only 6 of these 7 arguments (gridworld.py:719-722);
+// auto_value is never read (it only matters for OP_ALIGN, RewardEngine.cc:252).
+MFX_API int gridworld_add_reward_rule(void* game, int on, int* receiver, float* value, int n_receiver, bool is_terminal,
+                                      bool auto_value) {
+    (void)auto_value;
+    BattleEngine* e = MFX_ENV(game);
+    BattleEngine::Rule r;
+    r.on = on;
+    r.recv.assign(receiver, receiver + n_receiver);
+    r.val.assign(value, value + n_receiver);
+    r.terminal = is_terminal;
+    e->rules.push_back(std::move(r));
+    return 0;
+}
+
+// ---- batched device API (include/magent_amd.h) ---------------------------------------
+MFX_API int mfx_battle_set_num_envs(void* game, int n_envs) {
+    BattleEngine* e = MFX_ENV(game);
+    if (e->allocated) return mfx::fail("set_num_envs must precede the first reset");
+    if (n_envs < 1) return mfx::fail("n_envs must be >= 1");
+    e->E = n_envs;
+    return 0;
+}
+MFX_API int mfx_battle_set_stream(void* game, void* stream) {
+    BattleEngine* e = MFX_ENV(game);
+    if (e->own_stream && e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
+    e->stream = (hipStream_t)stream;
+    e->own_stream = false;
+    return 0;
+}
+MFX_API int mfx_battle_observe(void* game, int group, float* d_view, float* d_feature, int rowcap) {
+    MFX_GUARD(MFX_ENV(game)->observe(group, d_view, d_feature, rowcap));
+}
+MFX_API int mfx_battle_set_action(void* game, int group, const int* d_actions, int rowcap) {
+    MFX_GUARD(MFX_ENV(game)->set_action(group, d_actions, rowcap));
+}
+MFX_API int mfx_battle_step(void* game, int* d_done) { MFX_GUARD(MFX_ENV(game)->step(d_done)); }
+MFX_API int mfx_battle_get(void* game, int group, int what, void* d_out, int rowcap) {
+    MFX_GUARD(MFX_ENV(game)->get(group, what, d_out, rowcap));
+}
+MFX_API int mfx_battle_clear_dead(void* game) { MFX_GUARD(MFX_ENV(game)->clear_dead()); }
+MFX_API int mfx_battle_sync(void* game) {
+    BattleEngine* e = MFX_ENV(game);
+    if (!e->allocated) return 0;
+    MFX_HIP(hipStreamSynchronize(e->stream));
+    return e->check_err();
+}
+MFX_API int mfx_battle_group_capacity(void* game, int group, int* cap) {
+    BattleEngine* e = MFX_ENV(game);
+    if (group < 0 || group >= e->n_groups()) return mfx::fail("bad group");
+    *cap = e->allocated ? e->group_ub[group] : 0;
+    return 0;
+}
+
+}  // extern "C"

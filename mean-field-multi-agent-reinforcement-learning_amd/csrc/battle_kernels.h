@@ -1,0 +1,27 @@
+// battle_kernels.h -- host-side launchers of the Battle kernels (battle_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "battle_layout.h"
+
+namespace mfx {
+
+enum GetWhat : int { kGetNum = 0, kGetReward = 1, kGetId = 2, kGetAlive = 3, kGetPos = 4, kGetHp = 5 };
+
+size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n);
+size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap);
+
+hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st);
+hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
+                             const int* d_xs, const int* d_ys, int per_env_stride, hipStream_t st);
+hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
+                          float* d_view, float* d_feat, int rowcap, hipStream_t st);
+hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, const int* d_actions, int rowcap,
+                             hipStream_t st);
+hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State& s, int max_ids,
+                       uint32_t* d_sort_scratch, hipStream_t st);
+hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st);
+hipError_t launch_get(const GameParams* d_gp, const State& s, int g, int what, void* d_out, int rowcap,
+                      hipStream_t st);
+
+}  // namespace mfx

@@ -1,0 +1,736 @@
+// battle_kernels.hip -- HIP/CDNA4 (gfx950) kernels of the Battle gridworld.
+//
+// Every kernel owns whole environments: workgroup b works on env b (or on a chunk of
+// agents of env b for the observation kernel), so no inter-workgroup communication is
+// ever needed.  The order-dependent parts of GridWorld::step (LCG attack shuffle,
+// attack resolution, first-come move resolution -- GridWorld.cc:507-672) run on one
+// lane against an LDS copy of the env; everything order-free (starve, reward rules,
+// set_action classification, clear_dead compaction, observation extraction) is spread
+// over the workgroup.  Semantics follow the reference single-thread engine exactly;
+// see DESIGN.md for the per-kernel roofline.
+//
+// Compiled with -ffp-contract=off: every float op is the reference's own single
+// IEEE operation (no FMA contraction, correctly-rounded division).
+#include <hip/hip_runtime.h>
+
+#include "battle_layout.h"
+#include "battle_kernels.h"
+
+namespace mfx {
+
+// --------------------------------------------------------------------------- utils
+__device__ __forceinline__ uint32_t minstd_next(uint32_t x) {   // minstd_rand0, GridWorld.h:106
+    uint64_t p = (uint64_t)x * 16807u;
+    p = (p & 0x7FFFFFFFull) + (p >> 31);
+    if (p >= 0x7FFFFFFFull) p -= 0x7FFFFFFFull;
+    return (uint32_t)p;
+}
+
+__device__ __forceinline__ void set_err(const State& s, int code) { atomicCAS(s.err, 0, code); }
+
+// Exclusive scan of a 0/1 flag over the workgroup (blockDim multiple of 64, <= 1024).
+__device__ __forceinline__ int block_scan_flag(int flag, int* wave_tot, int& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const unsigned long long m = __ballot(flag);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wid] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) { const int c = wave_tot[w]; off += (w < wid) ? c : 0; tot += c; }
+    __syncthreads();
+    total = tot;
+    return off + pre;
+}
+
+__device__ __forceinline__ int cell_group_ch(int og, int g, int G, int per) {   // make_channel_trans
+    return 1 + per * ((og - g + G) % G);
+}
+
+// ------------------------------------------------------------------------- env view
+// Pointers to ONE env's state, either into LDS copies or straight into HBM slabs.
+struct EnvView {
+    uint16_t* cells;
+    uint32_t* xy;
+    float* hp;
+    float* next_r;
+    float* last_r;
+    int32_t* last_act;
+    int32_t* op_obj;
+    uint8_t* meta;
+    int32_t* grp_ids;      // [G][cap]
+    int32_t* grp_n;        // [G]
+    int32_t* grp_dead;     // [G]
+    float* grp_reward;     // [G]
+    int cap;
+};
+
+__device__ __forceinline__ EnvView global_view(const State& s, int e, int G) {
+    EnvView v;
+    const size_t a = (size_t)e * s.cap;
+    v.cells = s.cells + (size_t)e * s.cells_n;
+    v.xy = s.xy + a; v.hp = s.hp + a; v.next_r = s.next_r + a; v.last_r = s.last_r + a;
+    v.last_act = s.last_act + a; v.op_obj = s.op_obj + a; v.meta = s.meta + a;
+    v.grp_ids = s.grp_ids + (size_t)e * G * s.cap;
+    v.grp_n = s.grp_n + e * G; v.grp_dead = s.grp_dead + e * G; v.grp_reward = s.grp_reward + e * G;
+    v.cap = s.cap;
+    return v;
+}
+
+// ==================================================================================
+//  reset / add_agents
+// ==================================================================================
+// GridWorld::reset (GridWorld.cc:76-124) + Map::reset (Map.cc:23-47): border walls, no agents.
+__global__ void __launch_bounds__(256) k_reset(const GameParams* __restrict__ gp, State s) {
+    const int e = blockIdx.x, W = gp->W, H = gp->H, G = gp->n_groups;
+    uint16_t* cells = s.cells + (size_t)e * s.cells_n;
+    for (int c = threadIdx.x; c < W * H; c += blockDim.x) {
+        const int x = c % W, y = c / W;
+        cells[c] = (x == 0 || y == 0 || x == W - 1 || y == H - 1) ? kCellWall : kCellEmpty;
+    }
+    if (threadIdx.x < G) {
+        s.grp_n[e * G + threadIdx.x] = 0;
+        s.grp_dead[e * G + threadIdx.x] = 0;
+        s.grp_reward[e * G + threadIdx.x] = 0.0f;
+    }
+    if (threadIdx.x == 0) { s.id_counter[e] = 0; s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = 0; }
+}
+
+__device__ __forceinline__ bool is_blank(const uint16_t* cells, int W, int H, int x, int y, int self) {
+    // Map::is_blank_area for a 1x1 body (Map.cc:466-482)
+    if (x < 0 || y < 0 || x + 1 >= W || y + 1 >= H) return false;
+    const uint32_t c = cells[y * W + x];
+    return c == kCellEmpty || (int)c == self;
+}
+
+// One lane per env: placements are order-dependent (an occupied cell is skipped and the
+// id is not consumed -- GridWorld.cc:180-187).  method: 0 custom, 1 random, 2 fill.
+__global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int group, int n, int method,
+                             const int* __restrict__ xs, const int* __restrict__ ys, int per_env_stride) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= s.E) return;
+    const int W = gp->W, H = gp->H, G = gp->n_groups;
+    EnvView v = global_view(s, e, G);
+    const int* px = xs + (size_t)e * per_env_stride;
+    const int* py = ys + (size_t)e * per_env_stride;
+    uint32_t rng = s.rng[e];
+    int idc = s.id_counter[e];
+    auto place = [&](int x, int y) {
+        if (group < 0) {                                         // Map::add_wall (Map.cc:108-115)
+            if (x < 0 || y < 0 || x >= W || y >= H) return;
+            uint16_t& c = v.cells[y * W + x];
+            if (c == kCellEmpty || c == kCellWall) c = kCellWall;
+            return;
+        }
+        if (!is_blank(v.cells, W, H, x, y, -1)) return;
+        if (idc >= s.cap || idc >= 0xFFFE) { set_err(s, 2); return; }
+        const TypeParams& T = gp->type[group];
+        const int id = idc++;
+        v.cells[y * W + x] = (uint16_t)id;
+        v.xy[id] = (uint32_t)x | ((uint32_t)y << 16);
+        v.hp[id] = T.hp;
+        v.last_r[id] = 0.0f;                                     // Agent ctor + init_reward()
+        v.next_r[id] = T.step_reward;
+        v.last_act[id] = T.n_action;
+        v.op_obj[id] = -1;
+        v.meta[id] = (uint8_t)meta_make(0, kOpNull, group);
+        int& n = v.grp_n[group];
+        v.grp_ids[group * s.cap + n] = id;
+        ++n;
+    };
+    if (method == 0) {
+        for (int i = 0; i < n; ++i) place(px[i], py[i]);
+    } else if (method == 1) {                                    // Map::get_random_blank (Map.cc:49-63)
+        for (int i = 0; i < n; ++i) {
+            int x = 0, y = 0, tries = 0;
+            for (;;) {
+                rng = minstd_next(rng); x = (int)(rng % (uint32_t)(W - 1));
+                rng = minstd_next(rng); y = (int)(rng % (uint32_t)(H - 1));
+                if (is_blank(v.cells, W, H, x, y, -1)) break;
+                if (tries++ > W * H) { set_err(s, 3); break; }
+            }
+            place(x, y);
+        }
+    } else {                                                     // fill: xs = {x, y, w, h}
+        for (int x = px[0]; x < px[0] + px[2]; ++x)
+            for (int y = px[1]; y < px[1] + px[3]; ++y) place(x, y);
+    }
+    s.rng[e] = rng;
+    s.id_counter[e] = idc;
+}
+
+// ==================================================================================
+//  observation  (GridWorld::get_observation, GridWorld.cc:303-426; Map::extract_view,
+//  Map.cc:130-218).  Output rows are staged in LDS K agents at a time and streamed out
+//  as 16-byte coalesced stores.
+// ==================================================================================
+constexpr int kObsK = 4;          // agents per staging round (K*1183*4 B = 18.9 KB for Battle)
+
+struct ObsSmem {                  // LDS carve-up of the observation kernels
+    float* stage;                 // [kObsK][VH*VW*n_ch]
+    float* mm;                    // [G][VH*VW] minimap density
+    int* hist;                    // [G][VH*VW]
+    uint8_t* mask;                // [VH*VW]
+    float* type_hp;               // [G]
+};
+
+__device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView& v, const ObsSmem& sm,
+                                            int VW, int VH) {
+    const int G = gp.n_groups, NV = VW * VH;
+    const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
+    for (int i = threadIdx.x; i < G * NV; i += blockDim.x) sm.hist[i] = 0;
+    __syncthreads();
+    for (int j = 0; j < G; ++j) {
+        const int n = v.grp_n[j];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t p = v.xy[v.grp_ids[j * v.cap + i]];
+            const int x = p & 0xFFFF, y = p >> 16;
+            atomicAdd(&sm.hist[j * NV + (y / sh) * VW + x / sw], 1);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * NV; i += blockDim.x) {
+        const int j = i / NV;
+        const int n = v.grp_n[j];
+        // 0/0 gives the x86 default NaN (0xFFC00000) in the reference; reproduce its bits.
+        sm.mm[i] = n ? (float)sm.hist[i] / (float)n : __uint_as_float(0xFFC00000u);
+    }
+    __syncthreads();
+}
+
+// Fill the staging rows of agents [a0, a0+k) of group g, then stream them to out_view.
+__device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v, const ObsSmem& sm,
+                                         int g, int a0, int k, float* __restrict__ out_view,
+                                         float* __restrict__ out_feat) {
+    const TypeParams& T = gp.type[g];
+    const int W = gp.W, H = gp.H, G = gp.n_groups, NC = gp.n_ch;
+    const int VW = T.view_w, VH = T.view_h, NV = VW * VH, VF = NV * NC;
+    const int per = gp.minimap ? 3 : 2;
+    const int sw = (W + VW - 1) / VW, sh = (H + VH - 1) / VH;
+    const int32_t* ids = v.grp_ids + g * v.cap;
+    // ---- phase 1: one lane per (agent, view cell) writes that cell's NC channels
+    for (int p = threadIdx.x; p < k * NV; p += blockDim.x) {
+        const int al = p / NV, c = p - al * NV;
+        const int vy = c / VW, vx = c - vy * VW;
+        const int id = ids[a0 + al];
+        const uint32_t pos = v.xy[id];
+        const int ax = pos & 0xFFFF, ay = pos >> 16;
+        float* o = sm.stage + (size_t)al * VF + c * NC;
+        for (int ch = 0; ch < NC; ++ch) o[ch] = 0.0f;
+        const int mx = ax + T.view_x1 + vx, my = ay + T.view_y1 + vy;
+        if (sm.mask[c] && mx >= 0 && my >= 0 && mx < W && my < H) {
+            const uint32_t cv = v.cells[my * W + mx];
+            if (cv == kCellWall) {
+                o[0] = 1.0f;
+            } else if (cv != kCellEmpty) {
+                const int og = meta_group(v.meta[cv]);
+                const int ch = cell_group_ch(og, g, G, per);
+                o[ch] = 1.0f;
+                o[ch + 1] = v.hp[cv] / sm.type_hp[og];
+            }
+        }
+        if (gp.minimap) {
+            const bool self = (vy == ay / sh) && (vx == ax / sw);
+            for (int j = 0; j < G; ++j) {
+                const float m = sm.mm[j * NV + c];
+                o[cell_group_ch(j, g, G, per) + 2] = self ? m + 1.0f : m;
+            }
+        }
+    }
+    // ---- features (GridWorld.cc:411-421): written straight out, consecutive lanes = consecutive floats
+    const int F = gp.feat_size[g], emb = gp.emb, na = T.n_action;
+    for (int p = threadIdx.x; p < k * F; p += blockDim.x) {
+        const int al = p / F, f = p - al * F;
+        const int id = ids[a0 + al];
+        float val = 0.0f;
+        if (f < emb) val = (float)((id >> f) & 1);
+        if (f == emb + v.last_act[id]) val = 1.0f;
+        if (f == emb + na) val = v.last_r[id];
+        if (gp.minimap) {
+            const uint32_t pos = v.xy[id];
+            if (f == emb + na + 1) val = (float)(int)(pos & 0xFFFF) / (float)W;
+            if (f == emb + na + 2) val = (float)(int)(pos >> 16) / (float)H;
+        }
+        out_feat[(size_t)(a0 + al) * F + f] = val;
+    }
+    __syncthreads();
+    // ---- phase 2: stream k*VF floats; row a0 starts 16-B aligned when a0 % 4 == 0 (VF*4*4 % 16 == 0)
+    float* dst = out_view + (size_t)a0 * VF;
+    const int nf = k * VF;
+    if ((((uintptr_t)dst) & 15) == 0) {
+        const int n4 = nf >> 2;
+        const float4* src4 = reinterpret_cast<const float4*>(sm.stage);
+        float4* dst4 = reinterpret_cast<float4*>(dst);
+        for (int i = threadIdx.x; i < n4; i += blockDim.x) dst4[i] = src4[i];
+        for (int i = (n4 << 2) + threadIdx.x; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
+    } else {
+        for (int i = threadIdx.x; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, size_t& off) {
+    const TypeParams& T = gp.type[g];
+    const int NV = T.view_w * T.view_h, G = gp.n_groups;
+    ObsSmem sm;
+    sm.stage = reinterpret_cast<float*>(smem + off); off += (size_t)kObsK * NV * gp.n_ch * 4;
+    sm.mm = reinterpret_cast<float*>(smem + off);    off += (size_t)G * NV * 4;
+    sm.hist = reinterpret_cast<int*>(smem + off);    off += (size_t)G * NV * 4;
+    sm.type_hp = reinterpret_cast<float*>(smem + off); off += 16;
+    sm.mask = reinterpret_cast<uint8_t*>(smem + off); off += (NV + 15) & ~15;
+    return sm;
+}
+
+__device__ __forceinline__ void obs_prologue(const GameParams& gp, const ObsSmem& sm, int g) {
+    const TypeParams& T = gp.type[g];
+    const int NV = T.view_w * T.view_h;
+    for (int i = threadIdx.x; i < NV; i += blockDim.x) sm.mask[i] = T.view_mask[i];
+    if (threadIdx.x < gp.n_groups) sm.type_hp[threadIdx.x] = gp.type[threadIdx.x].hp;
+}
+
+// grid: (chunks, E).  Chunk c covers agents [c*chunk, (c+1)*chunk) of group g.
+// out_view: [E][rowcap][VH][VW][NC], out_feat: [E][rowcap][F]
+__global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ gpp, State s, int g, int chunk,
+                                                 float* __restrict__ out_view, float* __restrict__ out_feat,
+                                                 int rowcap, int cells_in_lds) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const GameParams& gp = *gpp;
+    const int e = blockIdx.y, G = gp.n_groups;
+    EnvView v = global_view(s, e, G);
+    const int n = v.grp_n[g];
+    const int a_begin = blockIdx.x * chunk;
+    if (a_begin >= n) return;
+    const int a_end = min(n, a_begin + chunk);
+    if (a_end > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
+    size_t off = 0;
+    ObsSmem sm = carve_obs(smem, gp, g, off);
+    if (cells_in_lds) {
+        uint16_t* lc = reinterpret_cast<uint16_t*>(smem + off);
+        const int n2 = s.cells_n;
+        for (int i = threadIdx.x; i < n2; i += blockDim.x) lc[i] = v.cells[i];
+        v.cells = lc;
+    }
+    obs_prologue(gp, sm, g);
+    obs_minimap(gp, v, sm, gp.type[g].view_w, gp.type[g].view_h);
+    const TypeParams& T = gp.type[g];
+    const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
+    float* ov = out_view + (size_t)e * rowcap * VF;
+    float* of = out_feat + (size_t)e * rowcap * gp.feat_size[g];
+    for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
+}
+
+// ==================================================================================
+//  set_action (GridWorld.cc:430-496): classify in call order and append to the buffers.
+// ==================================================================================
+__device__ __forceinline__ void set_action_group(const GameParams& gp, const State& s, EnvView& v, int g,
+                                                 const int* __restrict__ acts, uint32_t* atk, int& n_atk,
+                                                 uint32_t* mov, int& n_mov, int* wave_tot, int acap) {
+    const TypeParams& T = gp.type[g];
+    const int n = v.grp_n[g];
+    int base_a = n_atk, base_m = n_mov;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+        const int i = i0 + threadIdx.x;
+        int a = 0, id = 0, is_move = 0, is_atk = 0;
+        uint32_t bucket = kBucketBoundary;
+        if (i < n) {
+            id = v.grp_ids[g * v.cap + i];
+            a = acts[i];
+            if (a < 0 || a >= T.n_action) { set_err(s, 5); a = T.turn_base > 6 ? 6 : 0; }
+            v.last_act[id] = a;
+            is_move = a < T.turn_base;
+            is_atk = !is_move;
+            if (is_move && gp.large_map) {
+                const int x = v.xy[id] & 0xFFFF, xr = x % gp.band_w;
+                if (!(xr < 4 || xr > gp.band_w - 4)) bucket = (uint32_t)(x / gp.band_w);
+            }
+        }
+        int tot_m, tot_a;
+        const int rm = block_scan_flag(is_move, wave_tot, tot_m);
+        const int ra = block_scan_flag(is_atk, wave_tot, tot_a);
+        if (is_move && base_m + rm < acap) mov[base_m + rm] = ((uint32_t)id << 16) | ((uint32_t)a << 8) | bucket;
+        if (is_atk && base_a + ra < acap) atk[base_a + ra] = ((uint32_t)id << 8) | (uint32_t)(a - T.attack_base);
+        base_m += tot_m;
+        base_a += tot_a;
+    }
+    if (base_m > acap || base_a > acap) { if (threadIdx.x == 0) set_err(s, 6); }
+    __syncthreads();
+    if (threadIdx.x == 0) { n_atk = min(base_a, acap); n_mov = min(base_m, acap); }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_set_action(const GameParams* __restrict__ gp, State s, int g,
+                                                    const int* __restrict__ actions, int rowcap) {
+    __shared__ int wave_tot[16];
+    const int e = blockIdx.x;
+    EnvView v = global_view(s, e, gp->n_groups);
+    if (v.grp_n[g] > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
+    set_action_group(*gp, s, v, g, actions + (size_t)e * rowcap, s.atk + (size_t)e * s.acap, s.n_atk[e],
+                     s.mov + (size_t)e * s.acap, s.n_mov[e], wave_tot, s.acap);
+}
+
+// ==================================================================================
+//  step (GridWorld.cc:498-694)
+// ==================================================================================
+struct StepSmem {
+    int wave_tot[16];
+    int flags[8];       // [0..kMaxRules) rule triggers
+};
+
+__device__ __forceinline__ void do_attack_serial(const GameParams& gp, EnvView& v, uint32_t* atk, int n_atk) {
+    // shuffled order, strictly sequential (the reference loop is racy with OMP>1; OMP=1 semantics)
+    const int W = gp.W, H = gp.H;
+    for (int i = 0; i < n_atk; ++i) {
+        const uint32_t ent = atk[i];
+        const int id = (int)(ent >> 8), ai = (int)(ent & 0xFF);
+        uint32_t m = v.meta[id];
+        if (meta_dead(m)) continue;
+        const int g = meta_group(m);
+        const TypeParams& T = gp.type[g];
+        const uint32_t p = v.xy[id];
+        const int ox = (int)(p & 0xFFFF) + T.att_x_off + T.att_dx[ai];
+        const int oy = (int)(p >> 16) + T.att_y_off + T.att_dy[ai];
+        uint32_t cv = kCellEmpty;
+        if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
+        if (cv >= kCellWall) { v.next_r[id] += T.attack_penalty; continue; }       // blank
+        const uint32_t om = v.meta[cv];
+        const int og = meta_group(om);
+        if (!T.attack_in_group && og == g) { v.next_r[id] += T.attack_penalty; continue; }
+        const TypeParams& OT = gp.type[og];
+        float reward = 0.0f;
+        const float ohp = v.hp[cv] - T.damage;                                    // Agent::be_attack
+        v.hp[cv] = ohp;
+        if (ohp < 0.0f) {
+            v.meta[cv] = (uint8_t)meta_make(1, meta_op(om), og);
+            v.next_r[cv] = OT.dead_penalty;
+            m = meta_make(0, kOpKill, g);
+            v.op_obj[id] = (int)cv;
+            v.cells[oy * W + ox] = kCellEmpty;                                      // remove_agent
+            v.grp_dead[og] += 1;
+            const float h2 = v.hp[id] + OT.kill_supply;                             // add_hp
+            v.hp[id] = T.hp < h2 ? T.hp : h2;
+            reward = OT.kill_reward;
+        } else {
+            m = meta_make(0, kOpAttack, g);
+            v.op_obj[id] = (int)cv;
+        }
+        v.meta[id] = (uint8_t)m;
+        v.next_r[id] += reward + T.attack_penalty;
+    }
+}
+
+__device__ __forceinline__ void do_move_one(const GameParams& gp, EnvView& v, uint32_t ent) {
+    // GridWorld.cc:631-660 + Map::do_move (Map.cc:324-369), NORTH, 1x1
+    const int id = (int)(ent >> 16), mi = (int)((ent >> 8) & 0xFF);
+    const uint32_t m = v.meta[id];
+    if (meta_dead(m)) return;
+    const int W = gp.W, H = gp.H;
+    const TypeParams& T = gp.type[meta_group(m)];
+    const uint32_t p = v.xy[id];
+    const int x = p & 0xFFFF, y = p >> 16;
+    const int nx = x + T.move_dx[mi], ny = y + T.move_dy[mi];
+    if (nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) return;     // out of board: no collide
+    const uint32_t cv = v.cells[ny * W + nx];
+    if (cv == kCellEmpty || (int)cv == id) {
+        v.cells[y * W + x] = kCellEmpty;
+        v.cells[ny * W + nx] = (uint16_t)id;
+        v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
+    } else if (cv != kCellWall) {
+        v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(m));
+        v.op_obj[id] = (int)cv;
+    }
+}
+
+// Everything of GridWorld::step for one env, executed by the whole workgroup.
+// atk/mov/sorted: pending buffers (any address space); sorted has room for n_mov entries.
+__device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
+                         uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
+                         int& done_out) {
+    const int G = gp.n_groups;
+    // ---- shuffle + attack: one lane (GridWorld.cc:507-558)
+    if (threadIdx.x == 0) {
+        uint32_t x = rng;
+        for (int i = 0; i < n_atk; ++i) {
+            x = minstd_next(x);
+            const int j = (int)(x % (uint32_t)(i + 1));
+            const uint32_t t = atk[i]; atk[i] = atk[j]; atk[j] = t;
+        }
+        rng = x;
+        do_attack_serial(gp, v, atk, n_atk);
+    }
+    __syncthreads();
+    // ---- starve (GridWorld.cc:570-595): independent per agent
+    for (int g = 0; g < G; ++g) {
+        const TypeParams& T = gp.type[g];
+        const int n = v.grp_n[g];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int id = v.grp_ids[g * v.cap + i];
+            const uint32_t m = v.meta[id];
+            if (meta_dead(m)) continue;
+            if (T.step_recover > 0.0f) {
+                const float h2 = v.hp[id] + T.step_recover;
+                v.hp[id] = T.hp < h2 ? T.hp : h2;
+            } else {
+                const float h2 = v.hp[id] - (-T.step_recover);
+                v.hp[id] = h2;
+                if (h2 < 0.0f) {
+                    v.meta[id] = (uint8_t)(m | 1u);
+                    v.next_r[id] = T.dead_penalty;
+                    const uint32_t p = v.xy[id];
+                    v.cells[(p >> 16) * gp.W + (p & 0xFFFF)] = kCellEmpty;
+                    atomicAdd(&v.grp_dead[g], 1);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- move order: large map = band buffers 0..n_sep-1 then boundary (GridWorld.cc:662-672)
+    const uint32_t* order = mov;
+    if (gp.large_map) {
+        int base = 0;
+        for (int b = 0; b <= gp.n_sep; ++b) {
+            const uint32_t want = b < gp.n_sep ? (uint32_t)b : kBucketBoundary;
+            for (int i0 = 0; i0 < n_mov; i0 += blockDim.x) {
+                const int i = i0 + threadIdx.x;
+                const uint32_t ent = i < n_mov ? mov[i] : 0u;
+                const int f = i < n_mov && (ent & 0xFF) == want;
+                int tot;
+                const int r = block_scan_flag(f, sm.wave_tot, tot);
+                if (f) sorted[base + r] = ent;
+                base += tot;
+            }
+        }
+        __syncthreads();
+        order = sorted;
+    }
+    if (threadIdx.x == 0)
+        for (int i = 0; i < n_mov; ++i) do_move_one(gp, v, order[i]);
+    __syncthreads();
+    // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
+    for (int r = 0; r < gp.n_rules; ++r) {
+        const RuleParams& R = gp.rules[r];
+        const int n = v.grp_n[R.subj_group];
+        int obj_recv = 0;
+        for (int k = 0; k < R.n_recv; ++k) obj_recv |= R.recv_is_obj[k];
+        if (threadIdx.x == 0) sm.flags[r] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int id = v.grp_ids[R.subj_group * v.cap + i];
+            const uint32_t m = v.meta[id];
+            const int ob = v.op_obj[id];
+            if ((int)meta_op(m) != R.op || ob < 0 || (int)meta_group(v.meta[ob]) != R.obj_group) continue;
+            sm.flags[r] = 1;
+            for (int k = 0; k < R.n_recv; ++k)
+                if (!R.recv_is_obj[k]) v.next_r[id] += R.val[k];
+        }
+        __syncthreads();
+        if (obj_recv && threadIdx.x == 0) {       // object receivers: DFS order, one lane
+            for (int i = 0; i < n; ++i) {
+                const int id = v.grp_ids[R.subj_group * v.cap + i];
+                const uint32_t m = v.meta[id];
+                const int ob = v.op_obj[id];
+                if ((int)meta_op(m) != R.op || ob < 0 || (int)meta_group(v.meta[ob]) != R.obj_group) continue;
+                for (int k = 0; k < R.n_recv; ++k)
+                    if (R.recv_is_obj[k]) v.next_r[ob] += R.val[k];
+            }
+        }
+        __syncthreads();
+    }
+    // ---- done (GridWorld.cc:678-693)
+    if (threadIdx.x == 0) {
+        int live = 0;
+        for (int g = 0; g < G; ++g) live += (v.grp_n[g] - v.grp_dead[g]) > 0;
+        int d = live < G;
+        for (int r = 0; r < gp.n_rules; ++r) d |= sm.flags[r] && gp.rules[r].terminal;
+        done_out = d;
+    }
+    __syncthreads();
+}
+
+// Copy an env into LDS, run the step, copy back.  When `lds` is 0 the env is worked on
+// in place in HBM (maps / agent counts too large for LDS).
+__global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp, State s, int lds,
+                                              uint32_t* __restrict__ sort_scratch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ StepSmem sm;
+    const GameParams& gp = *gpp;
+    const int e = blockIdx.x, G = gp.n_groups;
+    EnvView gv = global_view(s, e, G);
+    EnvView v = gv;
+    const int nid = s.id_counter[e];
+    const int n_atk = s.n_atk[e], n_mov = s.n_mov[e];
+    uint32_t* atk = s.atk + (size_t)e * s.acap;
+    uint32_t* mov = s.mov + (size_t)e * s.acap;
+    uint32_t* sorted = sort_scratch + (size_t)e * s.acap;
+    if (lds) {
+        size_t off = 0;
+        auto carve = [&](size_t bytes) { char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+        v.cells = reinterpret_cast<uint16_t*>(carve((size_t)s.cells_n * 2));
+        v.xy = reinterpret_cast<uint32_t*>(carve((size_t)nid * 4));
+        v.hp = reinterpret_cast<float*>(carve((size_t)nid * 4));
+        v.next_r = reinterpret_cast<float*>(carve((size_t)nid * 4));
+        v.op_obj = reinterpret_cast<int32_t*>(carve((size_t)nid * 4));
+        v.meta = reinterpret_cast<uint8_t*>(carve((size_t)nid));
+        uint32_t* latk = reinterpret_cast<uint32_t*>(carve((size_t)n_atk * 4));
+        uint32_t* lmov = reinterpret_cast<uint32_t*>(carve((size_t)n_mov * 4));
+        uint32_t* lsort = reinterpret_cast<uint32_t*>(carve((size_t)(gp.large_map ? n_mov : 0) * 4));
+        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
+        for (int i = threadIdx.x; i < nid; i += blockDim.x) {
+            v.xy[i] = gv.xy[i]; v.hp[i] = gv.hp[i]; v.next_r[i] = gv.next_r[i];
+            v.op_obj[i] = gv.op_obj[i]; v.meta[i] = gv.meta[i];
+        }
+        for (int i = threadIdx.x; i < n_atk; i += blockDim.x) latk[i] = atk[i];
+        for (int i = threadIdx.x; i < n_mov; i += blockDim.x) lmov[i] = mov[i];
+        atk = latk; mov = lmov; sorted = lsort;
+        __syncthreads();
+    }
+    uint32_t rng = s.rng[e];
+    int done = 0;
+    step_env(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done);
+    if (lds) {
+        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
+        for (int i = threadIdx.x; i < nid; i += blockDim.x) {
+            gv.xy[i] = v.xy[i]; gv.hp[i] = v.hp[i]; gv.next_r[i] = v.next_r[i];
+            gv.op_obj[i] = v.op_obj[i]; gv.meta[i] = v.meta[i];
+        }
+    }
+    if (threadIdx.x == 0) {
+        s.rng[e] = rng;
+        s.n_atk[e] = 0;
+        s.n_mov[e] = 0;
+        s.done[e] = done;
+    }
+}
+
+// ==================================================================================
+//  clear_dead (GridWorld.cc:696-728): ordered compaction + Agent::init_reward
+// ==================================================================================
+__device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v, int* wave_tot) {
+    for (int g = 0; g < gp.n_groups; ++g) {
+        const float step_reward = gp.type[g].step_reward;
+        const int n = v.grp_n[g];
+        int32_t* ids = v.grp_ids + g * v.cap;
+        int base = 0;
+        for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+            const int i = i0 + threadIdx.x;
+            int id = -1, alive = 0;
+            if (i < n) { id = ids[i]; alive = !meta_dead(v.meta[id]); }
+            int tot;
+            const int r = block_scan_flag(alive, wave_tot, tot);
+            // in-place compaction is safe: destination index <= source index, and all reads of
+            // this round happened before the barrier inside block_scan_flag
+            if (alive) {
+                ids[base + r] = id;
+                v.last_r[id] = v.next_r[id];
+                v.next_r[id] = step_reward;
+                v.op_obj[id] = -1;
+                v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
+            }
+            base += tot;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) { v.grp_n[g] = base; v.grp_dead[g] = 0; v.grp_reward[g] = 0.0f; }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_clear_dead(const GameParams* __restrict__ gp, State s) {
+    __shared__ int wave_tot[16];
+    EnvView v = global_view(s, blockIdx.x, gp->n_groups);
+    clear_dead_env(*gp, v, wave_tot);
+}
+
+// ==================================================================================
+//  getters: reward (GridWorld.cc:760-770) and info num/id/pos/alive (GridWorld.cc:786-807)
+// ==================================================================================
+__global__ void __launch_bounds__(256) k_get(const GameParams* __restrict__ gp, State s, int g, int what,
+                                             void* __restrict__ out, int rowcap) {
+    const int e = blockIdx.x;
+    EnvView v = global_view(s, e, gp->n_groups);
+    const int n = v.grp_n[g];
+    if (what == kGetNum) { if (threadIdx.x == 0) reinterpret_cast<int*>(out)[e] = n; return; }
+    if (n > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
+    const int32_t* ids = v.grp_ids + g * v.cap;
+    const size_t o = (size_t)e * rowcap;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int id = ids[i];
+        switch (what) {
+            case kGetReward: reinterpret_cast<float*>(out)[o + i] = v.next_r[id] + v.grp_reward[g]; break;
+            case kGetId: reinterpret_cast<int*>(out)[o + i] = id; break;
+            case kGetAlive: reinterpret_cast<uint8_t*>(out)[o + i] = !meta_dead(v.meta[id]); break;
+            case kGetPos: {
+                const uint32_t p = v.xy[id];
+                reinterpret_cast<int*>(out)[2 * (o + i)] = (int)(p & 0xFFFF);
+                reinterpret_cast<int*>(out)[2 * (o + i) + 1] = (int)(p >> 16);
+            } break;
+            case kGetHp: reinterpret_cast<float*>(out)[o + i] = v.hp[id]; break;
+            default: break;
+        }
+    }
+}
+
+// ==================================================================================
+//  host-side launchers
+// ==================================================================================
+size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n) {
+    const TypeParams& T = gp.type[g];
+    const size_t NV = (size_t)T.view_w * T.view_h;
+    size_t b = (size_t)kObsK * NV * gp.n_ch * 4 + 2 * gp.n_groups * NV * 4 + 16 + ((NV + 15) & ~15);
+    if (cells_in_lds) b += (size_t)cells_n * 2;
+    return b;
+}
+
+size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    return r16((size_t)cells_n * 2) + 4 * r16((size_t)n_ids * 4) + r16(n_ids) + 2 * r16((size_t)acap * 4) +
+           (gp.large_map ? r16((size_t)acap * 4) : 0);
+}
+
+hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st) {
+    k_reset<<<s.E, 256, 0, st>>>(d_gp, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
+                             const int* d_xs, const int* d_ys, int per_env_stride, hipStream_t st) {
+    k_add_agents<<<(s.E + 63) / 64, 64, 0, st>>>(d_gp, s, group, n, method, d_xs, d_ys, per_env_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
+                          float* d_view, float* d_feat, int rowcap, hipStream_t st) {
+    const int chunk = 64;
+    const int chunks = max(1, (max_n + chunk - 1) / chunk);
+    const int cells_in_lds = (size_t)s.cells_n * 2 <= 32768;
+    const size_t smem = observe_smem_bytes(gp, g, cells_in_lds, s.cells_n);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    dim3 grid(chunks, s.E);
+    k_observe<<<grid, 256, smem, st>>>(d_gp, s, g, chunk, d_view, d_feat, rowcap, cells_in_lds);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, const int* d_actions, int rowcap,
+                             hipStream_t st) {
+    k_set_action<<<s.E, 256, 0, st>>>(d_gp, s, g, d_actions, rowcap);
+    return hipGetLastError();
+}
+
+hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State& s, int max_ids,
+                       uint32_t* d_sort_scratch, hipStream_t st) {
+    const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap);
+    const int lds = smem <= 96 * 1024;
+    k_step<<<s.E, 256, lds ? smem : 0, st>>>(d_gp, s, lds, d_sort_scratch);
+    return hipGetLastError();
+}
+
+hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st) {
+    k_clear_dead<<<s.E, 256, 0, st>>>(d_gp, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_get(const GameParams* d_gp, const State& s, int g, int what, void* d_out, int rowcap,
+                      hipStream_t st) {
+    k_get<<<s.E, 256, 0, st>>>(d_gp, s, g, what, d_out, rowcap);
+    return hipGetLastError();
+}
+
+}  // namespace mfx

@@ -1,0 +1,106 @@
+// battle_layout.h -- HBM layout of a batch of Battle gridworlds (shared host/device).
+//
+// One engine holds E independent environments with identical configuration (map size,
+// agent types, reward rules).  All per-env state is struct-of-arrays in HBM with a fixed
+// per-env stride, so a workgroup that owns env e touches only its own slabs:
+//
+//   cells     u16 [E][H*W]    0xFFFF empty, 0xFFFE wall, else the occupying agent's id
+//   agents (indexed by id, ids are dense 0..id_counter-1 within an episode, GridWorld.cc:184)
+//     xy        u32 [E][cap]   x | y << 16
+//     hp        f32 [E][cap]
+//     next_r    f32 [E][cap]   Agent::next_reward  (GridWorld.h:248)
+//     last_r    f32 [E][cap]   Agent::last_reward
+//     last_act  i32 [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145)
+//     op_obj    i32 [E][cap]   id of Agent::op_obj or -1
+//     meta      u8  [E][cap]   bit0 dead | bits1-2 last_op | bits4-5 group
+//   groups
+//     grp_ids   i32 [E][G][cap] the ordered agent vector of each group (Group::agents)
+//     grp_n, grp_dead i32 [E][G];  grp_reward f32 [E][G]
+//   id_counter i32 [E], rng u32 [E] (minstd_rand0 state, GridWorld.h:106)
+//   pending actions since the last step (GridWorld::set_action, GridWorld.cc:430-496)
+//     atk u32 [E][acap] = id << 8 | attack index      n_atk i32 [E]
+//     mov u32 [E][acap] = id << 16 | move index << 8 | bucket (0xFF = boundary buffer)
+//                                                     n_mov i32 [E]
+#pragma once
+#include <stdint.h>
+
+namespace mfx {
+
+constexpr int kMaxGroups = 4;
+constexpr int kMaxViewCells = 32 * 32;
+constexpr int kMaxRangeCount = 64;
+constexpr int kMaxRules = 8;
+constexpr int kMaxRecv = 4;
+constexpr uint16_t kCellEmpty = 0xFFFF;
+constexpr uint16_t kCellWall = 0xFFFE;
+constexpr uint32_t kBucketBoundary = 0xFF;
+
+// last_op encoding in meta bits 1-2
+enum : uint32_t { kOpNull = 0, kOpAttack = 1, kOpKill = 2, kOpCollide = 3 };
+// reference EventOp numbering (grid_def.h:17-23), used by the reward-rule ABI
+enum : int { kEvKill = 3, kEvCollide = 6, kEvAttack = 7 };
+
+struct TypeParams {                 // AgentType (AgentType.h:17-52), the fields the path reads
+    float hp, damage, step_recover, kill_supply;
+    float step_reward, kill_reward, dead_penalty, attack_penalty;
+    int attack_in_group;
+    int n_action, turn_base, attack_base;
+    int n_move, n_attack;
+    int view_w, view_h, view_x1, view_y1;      // view window relative to the agent (NORTH)
+    int att_x_off, att_y_off;
+    int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];
+    int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];
+    uint8_t view_mask[kMaxViewCells];          // Range::is_in, row-major [view_h][view_w]
+};
+
+struct RuleParams {                 // RewardRule on one binary event between two 'any' symbols
+    int op;                         // kOpAttack / kOpKill / kOpCollide
+    int subj_group, obj_group;
+    int n_recv;
+    int recv_is_obj[kMaxRecv];
+    float val[kMaxRecv];
+    int terminal;
+};
+
+struct GameParams {
+    int W, H, n_groups, minimap, emb, n_ch;
+    int large_map, n_sep, band_w;
+    int n_rules;
+    int feat_size[kMaxGroups];
+    TypeParams type[kMaxGroups];    // per group (Group::type)
+    RuleParams rules[kMaxRules];
+};
+
+struct State {                      // device pointers; every array is [E][stride]
+    int E, cap, acap, cells_n;      // cells_n = H*W
+    uint16_t* cells;
+    uint32_t* xy;
+    float* hp;
+    float* next_r;
+    float* last_r;
+    int32_t* last_act;
+    int32_t* op_obj;
+    uint8_t* meta;
+    int32_t* grp_ids;               // [E][G][cap]
+    int32_t* grp_n;                 // [E][G]
+    int32_t* grp_dead;              // [E][G]
+    float* grp_reward;              // [E][G]
+    int32_t* id_counter;            // [E]
+    uint32_t* rng;                  // [E]
+    uint32_t* atk;                  // [E][acap]
+    int32_t* n_atk;                 // [E]
+    uint32_t* mov;                  // [E][acap]
+    int32_t* n_mov;                 // [E]
+    int32_t* done;                  // [E]
+    int32_t* err;                   // [1] sticky device-side error code
+};
+
+// meta helpers
+__host__ __device__ inline uint32_t meta_dead(uint32_t m) { return m & 1u; }
+__host__ __device__ inline uint32_t meta_op(uint32_t m) { return (m >> 1) & 3u; }
+__host__ __device__ inline uint32_t meta_group(uint32_t m) { return (m >> 4) & 3u; }
+__host__ __device__ inline uint32_t meta_make(uint32_t dead, uint32_t op, uint32_t g) {
+    return dead | (op << 1) | (g << 4);
+}
+
+}  // namespace mfx

@@ -1,0 +1,82 @@
+"""Shared test helpers: library locations, fixture replay, parity assertions (test infrastructure)."""
+import json
+import os
+
+import numpy as np
+
+import battle_driver as bd
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "mean-field-multi-agent-reinforcement-learning_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+HIP_LIB = os.path.join(PKG, "build", "libmagent.so")
+ORACLE_LIB = os.path.join(REPO, "oracle", "build", "libbattle_oracle.so")
+REF_LIB = os.path.join(REPO, "oracle", "_ref", "libmagent_ref.so")
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "battle_manifest.json")) as f:
+        return json.load(f)
+
+
+def battle_env(lib_path, map_size):
+    import magent
+    lib = magent.load_library(lib_path)
+    env = magent.GridWorld("battle", map_size=map_size, lib=lib)
+    return env, env.get_handles()
+
+
+def unpack_actions(fx, prefix, n):
+    """Split the flat recorded actions back into per-step [a_g0, a_g1]."""
+    flat = fx[prefix + "actions"].astype(np.int32)
+    out, off = [], 0
+    for row in n:
+        step = []
+        for k in row:
+            step.append(flat[off:off + k])
+            off += k
+        out.append(step)
+    return out
+
+
+def placement_for(case, ep):
+    if ep["placement"] == "generate_map":
+        return bd.placement_generate_map(case["map_size"], ep["seed"])
+    n_side = int(ep["placement"].replace("blocks", ""))
+    return bd.placement_blocks(case["map_size"], n_side)
+
+
+def replay_case(lib_path, name, max_steps=None):
+    """Replay every episode of fixture `name` on the engine at lib_path; return mismatches."""
+    case = manifest()["cases"][name]
+    fx = np.load(os.path.join(GOLDEN, name + ".npz"))
+    env, handles = battle_env(lib_path, case["map_size"])
+    problems = []
+    for k, ep in enumerate(case["episodes"]):
+        p = "e%d_" % k
+        n = fx[p + "n"]
+        acts = unpack_actions(fx, p, n)
+        steps = len(n) if max_steps is None else min(len(n), max_steps)
+        rec = bd.run_episode(env, handles, placement_for(case, ep), steps, actions=acts, keep_raw=False)
+        problems += compare(rec, fx, p, steps, "%s ep%d" % (name, k))
+    del env
+    return problems
+
+
+def compare(rec, fx, p, steps, tag):
+    bad = []
+    if len(rec["n"]) != steps:
+        bad.append("%s: episode length %d != %d" % (tag, len(rec["n"]), steps))
+    for t in range(min(steps, len(rec["n"]))):
+        if list(rec["n"][t]) != list(fx[p + "n"][t]):
+            bad.append("%s step %d: n %s != %s" % (tag, t, rec["n"][t], fx[p + "n"][t]))
+            break
+        for key in ("sha_view", "sha_feat", "sha_ids", "sha_reward", "sha_alive", "sha_pos"):
+            for g in range(len(rec[key][t])):
+                if bytes(rec[key][t][g]) != fx[p + key][t, g].tobytes():
+                    bad.append("%s step %d group %d: %s differs" % (tag, t, g, key))
+        if list(rec["num_after"][t]) != list(fx[p + "num_after"][t]) or rec["done"][t] != bool(fx[p + "done"][t]):
+            bad.append("%s step %d: num/done differ" % (tag, t))
+        if bad:
+            break
+    return bad
