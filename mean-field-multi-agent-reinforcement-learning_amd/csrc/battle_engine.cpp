@@ -110,6 +110,7 @@ public:
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    bool stream_set = false;                          // a caller-provided stream (may be the null stream)
     GameParams gp{};
     GameParams* d_gp = nullptr;
     State s{};
@@ -123,6 +124,13 @@ public:
     DevBuf<float> st_view, st_feat, st_f32;
     DevBuf<int> st_i32, st_xs, st_ys;
     DevBuf<uint8_t> st_u8;
+    // fused rollout (bench / throughput path)
+    bool rollout_ready = false;
+    RolloutArgs ra{};
+    DevBuf<float> ro_view[kMaxGroups], ro_feat[kMaxGroups], ro_rewards, ro_return;
+    DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
+    DevBuf<double> ro_mean, ro_stats;
+    DevBuf<unsigned long long> ro_steps;
 
     ~BattleEngine() { release(); if (own_stream && stream) (void)hipStreamDestroy(stream); }
 
@@ -332,7 +340,7 @@ public:
             const int G = n_groups();
             if (!allocated) {
                 MFX_HIP_THROW(hipGetDevice(&device));
-                if (!stream) { MFX_HIP_THROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); own_stream = true; }
+                if (!stream_set) { MFX_HIP_THROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); own_stream = true; }
                 s.E = E;
                 s.cells_n = W * H;
                 alloc(s.cells, (size_t)E * W * H);
@@ -443,6 +451,92 @@ public:
     int clear_dead() {
         if (!allocated) return fail("clear_dead before reset");
         MFX_HIP(launch_clear_dead(d_gp, s, stream));
+        return 0;
+    }
+
+    // ------------------------------------------------------------------ fused rollout
+    // Template placement per group (host arrays, applied in group order at every episode start),
+    // followed by an immediate reset + placement of every env.
+    int rollout_init(const int* tmpl_n, const int* const* xs, const int* const* ys, int max_steps, float eps,
+                     uint32_t seed, int stagger) {
+        const int G = n_groups();
+        if (!allocated) MFX_CHECK(reset());
+        int total = 0, rowcap = 4, tcap = 1;
+        for (int g = 0; g < G; g++) { total += tmpl_n[g]; rowcap = std::max(rowcap, tmpl_n[g]); tcap = std::max(tcap, tmpl_n[g]); }
+        rowcap = (rowcap + 3) & ~3;                      // 16-B aligned rows (4 * 1183 floats)
+        for (int g = 0; g < G; g++)
+            if (gtype(g).n_action > 64) return fail("rollout: n_action must be <= 64");
+        try {
+            ensure_capacity(total, total);
+            const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+            if (smem > 160 * 1024)
+                return fail("rollout: env does not fit in LDS (%zu bytes); use the per-call API", smem);
+            std::vector<int> hx((size_t)G * tcap, 0), hy((size_t)G * tcap, 0);
+            for (int g = 0; g < G; g++)
+                for (int i = 0; i < tmpl_n[g]; i++) { hx[(size_t)g * tcap + i] = xs[g][i]; hy[(size_t)g * tcap + i] = ys[g][i]; }
+            ro_tx.ensure(hx.size()); ro_ty.ensure(hy.size());
+            MFX_HIP_THROW(hipMemcpy(ro_tx.p, hx.data(), sizeof(int) * hx.size(), hipMemcpyHostToDevice));
+            MFX_HIP_THROW(hipMemcpy(ro_ty.p, hy.data(), sizeof(int) * hy.size(), hipMemcpyHostToDevice));
+            RolloutArgs a{};
+            for (int g = 0; g < G; g++) {
+                const TypeParams& T = gp.type[g];
+                ro_view[g].ensure((size_t)E * rowcap * T.view_w * T.view_h * gp.n_ch);
+                ro_feat[g].ensure((size_t)E * rowcap * gp.feat_size[g]);
+                a.view[g] = ro_view[g].p; a.feat[g] = ro_feat[g].p;
+                a.tmpl_n[g] = tmpl_n[g];
+            }
+            int na = 0;
+            for (int g = 0; g < G; g++) na = std::max(na, gtype(g).n_action);
+            ro_actions.ensure((size_t)E * G * rowcap); ro_rewards.ensure((size_t)E * G * rowcap);
+            ro_mean.ensure((size_t)E * G * na); ro_return.ensure((size_t)E * G); ro_eplen.ensure(E);
+            ro_stats.ensure((size_t)E * 4); ro_steps.ensure(E);
+            MFX_HIP_THROW(hipMemset(ro_return.p, 0, sizeof(float) * E * G));
+            // stagger episode phases over envs: env e's first episode is cut at max_steps - e*max_steps/E,
+            // so after max_steps steps the batch cycles through every phase of an episode uniformly
+            std::vector<int32_t> phase((size_t)E);
+            for (int e = 0; e < E; e++) phase[e] = stagger ? (int32_t)((long long)e * max_steps / E) : 0;
+            MFX_HIP_THROW(hipMemcpy(ro_eplen.p, phase.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice));
+            MFX_HIP_THROW(hipMemset(ro_stats.p, 0, sizeof(double) * E * 4));
+            MFX_HIP_THROW(hipMemset(ro_steps.p, 0, sizeof(unsigned long long) * E));
+            a.rowcap = rowcap; a.actions = ro_actions.p; a.rewards = ro_rewards.p; a.mean_act = ro_mean.p;
+            a.ep_return = ro_return.p; a.ep_len = ro_eplen.p; a.stats = ro_stats.p; a.agent_steps = ro_steps.p;
+            a.tmpl_x = ro_tx.p; a.tmpl_y = ro_ty.p; a.tmpl_cap = tcap;
+            a.max_steps = max_steps; a.policy_seed = seed; a.step_index = 0; a.eps = eps;
+            ra = a;
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        MFX_CHECK(reset());
+        for (int g = 0; g < G; g++) MFX_CHECK(add_agents(g, tmpl_n[g], "custom", xs[g], ys[g]));
+        rollout_ready = true;
+        return 0;
+    }
+
+    int rollout_step(int n_steps) {
+        if (!rollout_ready) return fail("rollout_step before rollout_init");
+        for (int i = 0; i < n_steps; i++) {
+            MFX_HIP(launch_rollout(gp, d_gp, s, ra, stream));
+            ra.step_index++;
+        }
+        return 0;
+    }
+
+    int rollout_buffer(const char* name, int group, void** ptr, size_t* bytes) {
+        if (!rollout_ready) return fail("rollout_buffer before rollout_init");
+        const int G = n_groups();
+        if (group < 0 || group >= G) return fail("bad group");
+        const TypeParams& T = gp.type[group];
+        const size_t rc = ra.rowcap;
+        if (!strcmp(name, "view")) { *ptr = ra.view[group]; *bytes = E * rc * T.view_w * T.view_h * gp.n_ch * 4; }
+        else if (!strcmp(name, "feature")) { *ptr = ra.feat[group]; *bytes = E * rc * gp.feat_size[group] * 4; }
+        else if (!strcmp(name, "actions")) { *ptr = ra.actions; *bytes = (size_t)E * G * rc * 4; }
+        else if (!strcmp(name, "rewards")) { *ptr = ra.rewards; *bytes = (size_t)E * G * rc * 4; }
+        else if (!strcmp(name, "mean_action")) { *ptr = ra.mean_act; *bytes = ro_mean.n * 8; }
+        else if (!strcmp(name, "episode_return")) { *ptr = ra.ep_return; *bytes = (size_t)E * G * 4; }
+        else if (!strcmp(name, "stats")) { *ptr = ra.stats; *bytes = (size_t)E * 4 * 8; }
+        else if (!strcmp(name, "agent_steps")) { *ptr = ra.agent_steps; *bytes = (size_t)E * 8; }
+        else if (!strcmp(name, "group_num")) { *ptr = s.grp_n; *bytes = (size_t)E * G * 4; }
+        else return fail("unknown rollout buffer %s", name);
         return 0;
     }
 
@@ -613,6 +707,7 @@ MFX_API int mfx_battle_set_stream(void* game, void* stream) {
     if (e->own_stream && e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
     e->stream = (hipStream_t)stream;
     e->own_stream = false;
+    e->stream_set = true;
     return 0;
 }
 MFX_API int mfx_battle_observe(void* game, int group, float* d_view, float* d_feature, int rowcap) {
@@ -631,6 +726,34 @@ MFX_API int mfx_battle_sync(void* game) {
     if (!e->allocated) return 0;
     MFX_HIP(hipStreamSynchronize(e->stream));
     return e->check_err();
+}
+MFX_API int mfx_battle_rollout_init(void* game, const int* tmpl_n, const int* const* xs, const int* const* ys,
+                                    int max_steps, float eps, unsigned seed, int stagger) {
+    MFX_GUARD(MFX_ENV(game)->rollout_init(tmpl_n, xs, ys, max_steps, eps, seed, stagger));
+}
+MFX_API int mfx_battle_rollout_step(void* game, int n_steps) { MFX_GUARD(MFX_ENV(game)->rollout_step(n_steps)); }
+MFX_API int mfx_battle_rollout_buffer(void* game, const char* name, int group, void** ptr, size_t* bytes) {
+    MFX_GUARD(MFX_ENV(game)->rollout_buffer(name, group, ptr, bytes));
+}
+// Copy a rollout buffer (see rollout_buffer names) to dst (host or device pointer),
+// asynchronously on the engine stream; `bytes` may be smaller than the buffer.
+MFX_API int mfx_battle_rollout_copy(void* game, const char* name, int group, void* dst, size_t bytes) {
+    BattleEngine* e = MFX_ENV(game);
+    void* src = nullptr;
+    size_t n = 0;
+    MFX_CHECK(e->rollout_buffer(name, group, &src, &n));
+    if (bytes > n) return mfx::fail("rollout_copy: %zu bytes requested, buffer has %zu", bytes, n);
+    MFX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, e->stream));
+    return 0;
+}
+// Diagnostic build only: route k_rollout phase stamps ([E][16] u64 s_memtime) to d_buf.
+MFX_API int mfx_battle_set_stamp_buffer(void* d_buf) {
+    MFX_HIP(mfx::set_stamp_buffer((unsigned long long*)d_buf));
+    return 0;
+}
+MFX_API int mfx_battle_rollout_rowcap(void* game, int* rowcap) {
+    *rowcap = MFX_ENV(game)->ra.rowcap;
+    return 0;
 }
 MFX_API int mfx_battle_group_capacity(void* game, int group, int* cap) {
     BattleEngine* e = MFX_ENV(game);

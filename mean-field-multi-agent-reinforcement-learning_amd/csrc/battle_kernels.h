@@ -8,7 +8,7 @@ namespace mfx {
 
 enum GetWhat : int { kGetNum = 0, kGetReward = 1, kGetId = 2, kGetAlive = 3, kGetPos = 4, kGetHp = 5 };
 
-size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n);
+size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n, int cap);
 size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap);
 
 hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st);
@@ -21,6 +21,10 @@ hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, cons
 hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State& s, int max_ids,
                        uint32_t* d_sort_scratch, hipStream_t st);
 hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st);
+hipError_t set_stamp_buffer(unsigned long long* d_buf);
+size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap);
+hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
+                          hipStream_t st);
 hipError_t launch_get(const GameParams* d_gp, const State& s, int g, int what, void* d_out, int rowcap,
                       hipStream_t st);
 

@@ -18,6 +18,19 @@
 
 namespace mfx {
 
+// Diagnostic build only (-DMFX_STAMPS, build/libmagent_stamps.so): per-phase s_memtime deltas of
+// k_rollout go to a stamp buffer nobody else reads.  The real build compiles these to nothing.
+#ifdef MFX_STAMPS
+__device__ unsigned long long* g_stamps;
+#define MFX_STAMP(i)                                                                        \
+    do {                                                                                    \
+        __syncthreads();                                                                    \
+        if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define MFX_STAMP(i) do {} while (0)
+#endif
+
 // --------------------------------------------------------------------------- utils
 __device__ __forceinline__ uint32_t minstd_next(uint32_t x) {   // minstd_rand0, GridWorld.h:106
     uint64_t p = (uint64_t)x * 16807u;
@@ -164,27 +177,38 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
 //  as 16-byte coalesced stores.
 // ==================================================================================
 constexpr int kObsK = 4;          // agents per staging round (K*1183*4 B = 18.9 KB for Battle)
+constexpr int kMaxCh = 1 + 3 * kMaxGroups;
 
 struct ObsSmem {                  // LDS carve-up of the observation kernels
     float* stage;                 // [kObsK][VH*VW*n_ch]
     float* mm;                    // [G][VH*VW] minimap density
     int* hist;                    // [G][VH*VW]
+    uint16_t* bin;                // [cap] minimap cell of every agent id (this call)
     uint8_t* mask;                // [VH*VW]
     float* type_hp;               // [G]
 };
 
-__device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView& v, const ObsSmem& sm,
-                                            int VW, int VH) {
-    const int G = gp.n_groups, NV = VW * VH;
+// Battle fast path (builtin/config/battle.py): 13x13 view, 7 channels, 2 groups, minimap, 34
+// features.  kB = true folds every view/channel/feature dimension into a constant (no runtime
+// integer division in the inner loops); kB = false is the generic path for any other config.
+struct BattleShape { static constexpr int VW = 13, VH = 13, NC = 7, G = 2, F = 34; };
+
+template <bool kB>
+__device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView& v, const ObsSmem& sm) {
+    const TypeParams& T0 = gp.type[0];
+    const int VW = kB ? BattleShape::VW : T0.view_w, VH = kB ? BattleShape::VH : T0.view_h;
+    const int G = kB ? BattleShape::G : gp.n_groups, NV = VW * VH;
     const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
     for (int i = threadIdx.x; i < G * NV; i += blockDim.x) sm.hist[i] = 0;
     __syncthreads();
     for (int j = 0; j < G; ++j) {
         const int n = v.grp_n[j];
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint32_t p = v.xy[v.grp_ids[j * v.cap + i]];
-            const int x = p & 0xFFFF, y = p >> 16;
-            atomicAdd(&sm.hist[j * NV + (y / sh) * VW + x / sw], 1);
+            const int id = v.grp_ids[j * v.cap + i];
+            const uint32_t p = v.xy[id];
+            const int b = ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw;
+            sm.bin[id] = (uint16_t)b;
+            atomicAdd(&sm.hist[j * NV + b], 1);
         }
     }
     __syncthreads();
@@ -198,46 +222,61 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
 }
 
 // Fill the staging rows of agents [a0, a0+k) of group g, then stream them to out_view.
+template <bool kB>
 __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v, const ObsSmem& sm,
                                          int g, int a0, int k, float* __restrict__ out_view,
                                          float* __restrict__ out_feat) {
     const TypeParams& T = gp.type[g];
-    const int W = gp.W, H = gp.H, G = gp.n_groups, NC = gp.n_ch;
-    const int VW = T.view_w, VH = T.view_h, NV = VW * VH, VF = NV * NC;
-    const int per = gp.minimap ? 3 : 2;
-    const int sw = (W + VW - 1) / VW, sh = (H + VH - 1) / VH;
+    const int W = gp.W, H = gp.H;
+    const int G = kB ? BattleShape::G : gp.n_groups, NC = kB ? BattleShape::NC : gp.n_ch;
+    const int VW = kB ? BattleShape::VW : T.view_w, VH = kB ? BattleShape::VH : T.view_h;
+    const int NV = VW * VH, VF = NV * NC;
+    const bool MM = kB ? true : gp.minimap != 0;
+    const int per = MM ? 3 : 2;
     const int32_t* ids = v.grp_ids + g * v.cap;
-    // ---- phase 1: one lane per (agent, view cell) writes that cell's NC channels
+    // ---- phase 1: one lane per (agent, view cell) computes that cell's NC channels
     for (int p = threadIdx.x; p < k * NV; p += blockDim.x) {
         const int al = p / NV, c = p - al * NV;
         const int vy = c / VW, vx = c - vy * VW;
         const int id = ids[a0 + al];
         const uint32_t pos = v.xy[id];
-        const int ax = pos & 0xFFFF, ay = pos >> 16;
-        float* o = sm.stage + (size_t)al * VF + c * NC;
-        for (int ch = 0; ch < NC; ++ch) o[ch] = 0.0f;
-        const int mx = ax + T.view_x1 + vx, my = ay + T.view_y1 + vy;
+        float o[kMaxCh];
+#pragma unroll
+        for (int q = 0; q < kMaxCh; ++q) o[q] = 0.0f;
+        const int mx = (int)(pos & 0xFFFF) + T.view_x1 + vx, my = (int)(pos >> 16) + T.view_y1 + vy;
         if (sm.mask[c] && mx >= 0 && my >= 0 && mx < W && my < H) {
             const uint32_t cv = v.cells[my * W + mx];
             if (cv == kCellWall) {
                 o[0] = 1.0f;
             } else if (cv != kCellEmpty) {
                 const int og = meta_group(v.meta[cv]);
-                const int ch = cell_group_ch(og, g, G, per);
-                o[ch] = 1.0f;
-                o[ch + 1] = v.hp[cv] / sm.type_hp[og];
+                const int ch = 1 + per * ((og - g + G) % G);
+                const float hn = v.hp[cv] / sm.type_hp[og];
+#pragma unroll
+                for (int q = 0; q < kMaxCh; ++q) {
+                    if (q == ch) o[q] = 1.0f;
+                    if (q == ch + 1) o[q] = hn;
+                }
             }
         }
-        if (gp.minimap) {
-            const bool self = (vy == ay / sh) && (vx == ax / sw);
+        if (MM) {
+            const bool self = c == (int)sm.bin[id];
             for (int j = 0; j < G; ++j) {
                 const float m = sm.mm[j * NV + c];
-                o[cell_group_ch(j, g, G, per) + 2] = self ? m + 1.0f : m;
+                const int ch = 3 + per * ((j - g + G) % G);
+#pragma unroll
+                for (int q = 0; q < kMaxCh; ++q)
+                    if (q == ch) o[q] = self ? m + 1.0f : m;
             }
         }
+        float* dst = sm.stage + (size_t)al * VF + c * NC;
+#pragma unroll
+        for (int q = 0; q < kMaxCh; ++q)
+            if (q < NC) dst[q] = o[q];
     }
     // ---- features (GridWorld.cc:411-421): written straight out, consecutive lanes = consecutive floats
-    const int F = gp.feat_size[g], emb = gp.emb, na = T.n_action;
+    const int F = kB ? BattleShape::F : gp.feat_size[g];
+    const int emb = gp.emb, na = T.n_action;
     for (int p = threadIdx.x; p < k * F; p += blockDim.x) {
         const int al = p / F, f = p - al * F;
         const int id = ids[a0 + al];
@@ -245,7 +284,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
         if (f < emb) val = (float)((id >> f) & 1);
         if (f == emb + v.last_act[id]) val = 1.0f;
         if (f == emb + na) val = v.last_r[id];
-        if (gp.minimap) {
+        if (MM) {
             const uint32_t pos = v.xy[id];
             if (f == emb + na + 1) val = (float)(int)(pos & 0xFFFF) / (float)W;
             if (f == emb + na + 2) val = (float)(int)(pos >> 16) / (float)H;
@@ -268,15 +307,32 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     __syncthreads();
 }
 
-__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, size_t& off) {
+__host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
+    if (gp.n_groups != BattleShape::G || !gp.minimap || gp.n_ch != BattleShape::NC) return false;
+    for (int g = 0; g < gp.n_groups; ++g)
+        if (gp.type[g].view_w != BattleShape::VW || gp.type[g].view_h != BattleShape::VH ||
+            gp.feat_size[g] != BattleShape::F)
+            return false;
+    return true;
+}
+
+__host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int cap) {
+    const size_t NV = (size_t)gp.type[g].view_w * gp.type[g].view_h;
+    return (size_t)kObsK * NV * gp.n_ch * 4 + 2 * (((size_t)gp.n_groups * NV * 4 + 15) & ~(size_t)15) +
+           (((size_t)cap * 2 + 15) & ~(size_t)15) + 16 + ((NV + 15) & ~(size_t)15);
+}
+
+__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, int cap, size_t& off) {
     const TypeParams& T = gp.type[g];
-    const int NV = T.view_w * T.view_h, G = gp.n_groups;
+    const size_t NV = (size_t)T.view_w * T.view_h, G = gp.n_groups;
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     ObsSmem sm;
     sm.stage = reinterpret_cast<float*>(smem + off); off += (size_t)kObsK * NV * gp.n_ch * 4;
-    sm.mm = reinterpret_cast<float*>(smem + off);    off += (size_t)G * NV * 4;
-    sm.hist = reinterpret_cast<int*>(smem + off);    off += (size_t)G * NV * 4;
+    sm.mm = reinterpret_cast<float*>(smem + off);    off += r16(G * NV * 4);
+    sm.hist = reinterpret_cast<int*>(smem + off);    off += r16(G * NV * 4);
+    sm.bin = reinterpret_cast<uint16_t*>(smem + off); off += r16((size_t)cap * 2);
     sm.type_hp = reinterpret_cast<float*>(smem + off); off += 16;
-    sm.mask = reinterpret_cast<uint8_t*>(smem + off); off += (NV + 15) & ~15;
+    sm.mask = reinterpret_cast<uint8_t*>(smem + off); off += r16(NV);
     return sm;
 }
 
@@ -289,6 +345,7 @@ __device__ __forceinline__ void obs_prologue(const GameParams& gp, const ObsSmem
 
 // grid: (chunks, E).  Chunk c covers agents [c*chunk, (c+1)*chunk) of group g.
 // out_view: [E][rowcap][VH][VW][NC], out_feat: [E][rowcap][F]
+template <bool kB>
 __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ gpp, State s, int g, int chunk,
                                                  float* __restrict__ out_view, float* __restrict__ out_feat,
                                                  int rowcap, int cells_in_lds) {
@@ -302,7 +359,7 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     const int a_end = min(n, a_begin + chunk);
     if (a_end > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
     size_t off = 0;
-    ObsSmem sm = carve_obs(smem, gp, g, off);
+    ObsSmem sm = carve_obs(smem, gp, g, s.cap, off);
     if (cells_in_lds) {
         uint16_t* lc = reinterpret_cast<uint16_t*>(smem + off);
         const int n2 = s.cells_n;
@@ -310,12 +367,12 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
         v.cells = lc;
     }
     obs_prologue(gp, sm, g);
-    obs_minimap(gp, v, sm, gp.type[g].view_w, gp.type[g].view_h);
+    obs_minimap<kB>(gp, v, sm);
     const TypeParams& T = gp.type[g];
     const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
     float* ov = out_view + (size_t)e * rowcap * VF;
     float* of = out_feat + (size_t)e * rowcap * gp.feat_size[g];
-    for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
+    for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows<kB>(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
 }
 
 // ==================================================================================
@@ -669,12 +726,264 @@ __global__ void __launch_bounds__(256) k_get(const GameParams* __restrict__ gp, 
 }
 
 // ==================================================================================
+//  fused rollout step: the whole reference training-loop step for one env per workgroup,
+//  env state resident in LDS for the duration of the launch (senario_battle.play :96-171:
+//  get_observation x G -> policy -> set_action x G -> step -> get_reward -> mean action ->
+//  clear_dead, plus episode restart at done / max_steps).
+// ==================================================================================
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {      // murmur3 finalizer
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
+// Synthetic rush policy of SURVEY.md 8(d) (tests/battle_driver.rush_policy): attack the
+// first attack cell (index order = view2attack row-major order) holding an enemy, else move
+// 2 cells toward the map centre; with probability eps a uniform random action instead.
+__device__ __forceinline__ int rush_action(const GameParams& gp, const EnvView& v, int g, int id, uint32_t key,
+                                           float eps) {
+    const TypeParams& T = gp.type[g];
+    const uint32_t p = v.xy[id];
+    const int x = p & 0xFFFF, y = p >> 16;
+    int a = ((float)x / (float)gp.W < 0.5f) ? 8 : 4;
+    if (a >= T.turn_base) a = T.turn_base - 1;
+    for (int k = 0; k < T.n_attack; ++k) {
+        const int ox = x + T.att_x_off + T.att_dx[k], oy = y + T.att_y_off + T.att_dy[k];
+        if (ox < 0 || oy < 0 || ox >= gp.W || oy >= gp.H) continue;
+        const uint32_t c = v.cells[oy * gp.W + ox];
+        if (c < kCellWall && (int)meta_group(v.meta[c]) != g) { a = T.attack_base + k; break; }
+    }
+    const uint32_t h = mix32(key);
+    if ((float)(h >> 8) * (1.0f / 16777216.0f) < eps) a = (int)(mix32(h ^ 0x68E31DA4u) % (uint32_t)T.n_action);
+    return a;
+}
+
+__device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-order reduction
+    red[threadIdx.x] = x;
+    __syncthreads();
+    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+}
+
+size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const int G = gp.n_groups;
+    size_t b = r16((size_t)cells_n * 2);
+    b += 6 * r16((size_t)cap * 4) + r16(cap);             // xy hp next_r last_r last_act op_obj + meta
+    b += r16((size_t)G * cap * 4) * 2;                     // grp_ids + policy actions
+    b += 3 * r16((size_t)acap * 4);                        // atk mov sorted
+    b += 4 * r16(G * 4) + r16(256 * 4) + r16((size_t)G * 64 * 4);   // counts, reduction, action histogram
+    b += obs_smem_core(gp, 0, cap);
+    return b;
+}
+
+template <bool kB>
+__global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ gpp, State s, RolloutArgs ra) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ StepSmem sm;
+    __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 2 id_counter, 3 done
+    const GameParams& gp = *gpp;
+    const int e = blockIdx.x, G = gp.n_groups, cap = s.cap, acap = s.acap;
+    EnvView gv = global_view(s, e, G);
+    // ---------------- carve LDS
+    size_t off = 0;
+    auto carve = [&](size_t bytes) { char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+    EnvView v;
+    v.cap = cap;
+    v.cells = reinterpret_cast<uint16_t*>(carve((size_t)s.cells_n * 2));
+    v.xy = reinterpret_cast<uint32_t*>(carve((size_t)cap * 4));
+    v.hp = reinterpret_cast<float*>(carve((size_t)cap * 4));
+    v.next_r = reinterpret_cast<float*>(carve((size_t)cap * 4));
+    v.last_r = reinterpret_cast<float*>(carve((size_t)cap * 4));
+    v.last_act = reinterpret_cast<int32_t*>(carve((size_t)cap * 4));
+    v.op_obj = reinterpret_cast<int32_t*>(carve((size_t)cap * 4));
+    v.meta = reinterpret_cast<uint8_t*>(carve((size_t)cap));
+    v.grp_ids = reinterpret_cast<int32_t*>(carve((size_t)G * cap * 4));
+    int32_t* act = reinterpret_cast<int32_t*>(carve((size_t)G * cap * 4));
+    uint32_t* atk = reinterpret_cast<uint32_t*>(carve((size_t)acap * 4));
+    uint32_t* mov = reinterpret_cast<uint32_t*>(carve((size_t)acap * 4));
+    uint32_t* sorted = reinterpret_cast<uint32_t*>(carve((size_t)acap * 4));
+    v.grp_n = reinterpret_cast<int32_t*>(carve(G * 4));
+    v.grp_dead = reinterpret_cast<int32_t*>(carve(G * 4));
+    v.grp_reward = reinterpret_cast<float*>(carve(G * 4));
+    int32_t* n_before = reinterpret_cast<int32_t*>(carve(G * 4));
+    float* red = reinterpret_cast<float*>(carve(256 * 4));
+    int* ahist = reinterpret_cast<int*>(carve((size_t)G * 64 * 4));
+    ObsSmem osm = carve_obs(smem, gp, 0, cap, off);
+    MFX_STAMP(0);
+    // ---------------- load the env
+    const int nid = s.id_counter[e];
+    if ((s.cells_n & 7) == 0) {   // per-env slab is 16-B aligned: move 8 cells per lane
+        for (int i = threadIdx.x; i < (s.cells_n >> 3); i += blockDim.x)
+            reinterpret_cast<uint4*>(v.cells)[i] = reinterpret_cast<const uint4*>(gv.cells)[i];
+    } else if ((s.cells_n & 1) == 0) {
+        for (int i = threadIdx.x; i < (s.cells_n >> 1); i += blockDim.x)
+            reinterpret_cast<uint32_t*>(v.cells)[i] = reinterpret_cast<const uint32_t*>(gv.cells)[i];
+    } else {
+        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
+    }
+    for (int i = threadIdx.x; i < nid; i += blockDim.x) {
+        v.xy[i] = gv.xy[i]; v.hp[i] = gv.hp[i]; v.next_r[i] = gv.next_r[i]; v.last_r[i] = gv.last_r[i];
+        v.last_act[i] = gv.last_act[i]; v.op_obj[i] = gv.op_obj[i]; v.meta[i] = gv.meta[i];
+    }
+    if (threadIdx.x < G) {
+        v.grp_n[threadIdx.x] = gv.grp_n[threadIdx.x];
+        v.grp_dead[threadIdx.x] = gv.grp_dead[threadIdx.x];
+        v.grp_reward[threadIdx.x] = gv.grp_reward[threadIdx.x];
+    }
+    __syncthreads();
+    for (int g = 0; g < G; ++g)
+        for (int i = threadIdx.x; i < v.grp_n[g]; i += blockDim.x) v.grp_ids[g * cap + i] = gv.grp_ids[g * cap + i];
+    if (threadIdx.x == 0) {
+        misc[0] = 0; misc[1] = 0;
+        unsigned long long tot = 0;
+        for (int g = 0; g < G; ++g) { n_before[g] = v.grp_n[g]; tot += (unsigned)v.grp_n[g]; }
+        ra.agent_steps[e] += tot;
+    }
+    __syncthreads();
+    MFX_STAMP(1);
+    // ---------------- get_observation for every group
+    obs_minimap<kB>(gp, v, osm);
+    MFX_STAMP(2);
+    for (int g = 0; g < G; ++g) {
+        obs_prologue(gp, osm, g);
+        __syncthreads();
+        const TypeParams& T = gp.type[g];
+        const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
+        float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
+        float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
+        const int n = min(v.grp_n[g], ra.rowcap);
+        for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
+    }
+    MFX_STAMP(3);
+    // ---------------- policy + mean action (former_act_prob)
+    for (int g = 0; g < G; ++g) {
+        const int n = v.grp_n[g], na = gp.type[g].n_action;
+        for (int i = threadIdx.x; i < 64; i += blockDim.x) ahist[g * 64 + i] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int id = v.grp_ids[g * cap + i];
+            const uint32_t key = ra.policy_seed ^ mix32(ra.step_index * 0x9E3779B9u + (uint32_t)e * 0x632BE5ABu) ^
+                                 mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
+            const int a = rush_action(gp, v, g, id, key, ra.eps);
+            act[g * cap + i] = a;
+            if (i < ra.rowcap) ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
+            atomicAdd(&ahist[g * 64 + a], 1);
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < na; k += blockDim.x)
+            ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[g * 64 + k] / (double)n : 0.0;
+    }
+    MFX_STAMP(4);
+    // ---------------- set_action (group order) and step
+    for (int g = 0; g < G; ++g) set_action_group(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
+    MFX_STAMP(5);
+    uint32_t rng = s.rng[e];
+    int done = 0;
+    step_env(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done);
+    MFX_STAMP(6);
+    // ---------------- get_reward, episode return, kills
+    float kills = 0.0f;
+    for (int g = 0; g < G; ++g) {
+        const int n = v.grp_n[g];
+        float part = 0.0f;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const float r = v.next_r[v.grp_ids[g * cap + i]] + v.grp_reward[g];
+            if (i < ra.rowcap) ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
+            part += r;
+        }
+        const float tot = block_sum(part, red);
+        if (threadIdx.x == 0) { ra.ep_return[e * G + g] += tot; kills += (float)v.grp_dead[g]; }
+    }
+    MFX_STAMP(7);
+    // ---------------- clear_dead
+    clear_dead_env(gp, v, sm.wave_tot);
+    MFX_STAMP(8);
+    // ---------------- episode end -> reset + re-place the template (env.reset + add_agents)
+    if (threadIdx.x == 0) {
+        double* st = ra.stats + (size_t)e * 4;
+        st[3] += kills;
+        int len = ra.ep_len[e] + 1;
+        if (done || len >= ra.max_steps) {
+            st[0] += 1.0;
+            st[1] += ra.ep_return[e * G + 0];
+            st[2] += G > 1 ? ra.ep_return[e * G + 1] : 0.0f;
+            for (int g = 0; g < G; ++g) ra.ep_return[e * G + g] = 0.0f;
+            len = 0;
+            misc[3] = 1;
+        } else {
+            misc[3] = 0;
+        }
+        ra.ep_len[e] = len;
+        s.rng[e] = rng;
+        s.done[e] = done;
+    }
+    __syncthreads();
+    int id_counter = nid;
+    if (misc[3]) {
+        const int W = gp.W, H = gp.H;
+        for (int c = threadIdx.x; c < W * H; c += blockDim.x) {
+            const int x = c % W, y = c / W;
+            v.cells[c] = (x == 0 || y == 0 || x == W - 1 || y == H - 1) ? kCellWall : kCellEmpty;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int idc = 0;
+            for (int g = 0; g < G; ++g) {
+                const TypeParams& T = gp.type[g];
+                v.grp_n[g] = 0; v.grp_dead[g] = 0; v.grp_reward[g] = 0.0f;
+                for (int i = 0; i < ra.tmpl_n[g]; ++i) {
+                    const int x = ra.tmpl_x[g * ra.tmpl_cap + i], y = ra.tmpl_y[g * ra.tmpl_cap + i];
+                    if (!is_blank(v.cells, W, H, x, y, -1) || idc >= cap) continue;
+                    const int id = idc++;
+                    v.cells[y * W + x] = (uint16_t)id;
+                    v.xy[id] = (uint32_t)x | ((uint32_t)y << 16);
+                    v.hp[id] = T.hp; v.last_r[id] = 0.0f; v.next_r[id] = T.step_reward;
+                    v.last_act[id] = T.n_action; v.op_obj[id] = -1;
+                    v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
+                    v.grp_ids[g * cap + v.grp_n[g]++] = id;
+                }
+            }
+            misc[2] = idc;
+        }
+        __syncthreads();
+        id_counter = misc[2];
+    }
+    MFX_STAMP(9);
+    // ---------------- write the env back
+    if ((s.cells_n & 7) == 0) {
+        for (int i = threadIdx.x; i < (s.cells_n >> 3); i += blockDim.x)
+            reinterpret_cast<uint4*>(gv.cells)[i] = reinterpret_cast<const uint4*>(v.cells)[i];
+    } else if ((s.cells_n & 1) == 0) {
+        for (int i = threadIdx.x; i < (s.cells_n >> 1); i += blockDim.x)
+            reinterpret_cast<uint32_t*>(gv.cells)[i] = reinterpret_cast<const uint32_t*>(v.cells)[i];
+    } else {
+        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
+    }
+    for (int i = threadIdx.x; i < id_counter; i += blockDim.x) {
+        gv.xy[i] = v.xy[i]; gv.hp[i] = v.hp[i]; gv.next_r[i] = v.next_r[i]; gv.last_r[i] = v.last_r[i];
+        gv.last_act[i] = v.last_act[i]; gv.op_obj[i] = v.op_obj[i]; gv.meta[i] = v.meta[i];
+    }
+    for (int g = 0; g < G; ++g)
+        for (int i = threadIdx.x; i < v.grp_n[g]; i += blockDim.x) gv.grp_ids[g * cap + i] = v.grp_ids[g * cap + i];
+    if (threadIdx.x < G) {
+        gv.grp_n[threadIdx.x] = v.grp_n[threadIdx.x];
+        gv.grp_dead[threadIdx.x] = v.grp_dead[threadIdx.x];
+        gv.grp_reward[threadIdx.x] = v.grp_reward[threadIdx.x];
+    }
+    if (threadIdx.x == 0) { s.id_counter[e] = id_counter; s.n_atk[e] = 0; s.n_mov[e] = 0; }
+    MFX_STAMP(10);
+}
+
+// ==================================================================================
 //  host-side launchers
 // ==================================================================================
-size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n) {
-    const TypeParams& T = gp.type[g];
-    const size_t NV = (size_t)T.view_w * T.view_h;
-    size_t b = (size_t)kObsK * NV * gp.n_ch * 4 + 2 * gp.n_groups * NV * 4 + 16 + ((NV + 15) & ~15);
+size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n, int cap) {
+    size_t b = obs_smem_core(gp, g, cap);
     if (cells_in_lds) b += (size_t)cells_n * 2;
     return b;
 }
@@ -701,10 +1010,13 @@ hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const St
     const int chunk = 64;
     const int chunks = max(1, (max_n + chunk - 1) / chunk);
     const int cells_in_lds = (size_t)s.cells_n * 2 <= 32768;
-    const size_t smem = observe_smem_bytes(gp, g, cells_in_lds, s.cells_n);
+    const size_t smem = observe_smem_bytes(gp, g, cells_in_lds, s.cells_n, s.cap);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     dim3 grid(chunks, s.E);
-    k_observe<<<grid, 256, smem, st>>>(d_gp, s, g, chunk, d_view, d_feat, rowcap, cells_in_lds);
+    if (is_battle_shape(gp))
+        k_observe<true><<<grid, 256, smem, st>>>(d_gp, s, g, chunk, d_view, d_feat, rowcap, cells_in_lds);
+    else
+        k_observe<false><<<grid, 256, smem, st>>>(d_gp, s, g, chunk, d_view, d_feat, rowcap, cells_in_lds);
     return hipGetLastError();
 }
 
@@ -724,6 +1036,26 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
 
 hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st) {
     k_clear_dead<<<s.E, 256, 0, st>>>(d_gp, s);
+    return hipGetLastError();
+}
+
+hipError_t set_stamp_buffer(unsigned long long* d_buf) {
+#ifdef MFX_STAMPS
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &d_buf, sizeof(d_buf));
+#else
+    (void)d_buf;
+    return hipErrorNotSupported;
+#endif
+}
+
+hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
+                          hipStream_t st) {
+    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    if (is_battle_shape(gp))
+        k_rollout<true><<<s.E, 256, smem, st>>>(d_gp, s, ra);
+    else
+        k_rollout<false><<<s.E, 256, smem, st>>>(d_gp, s, ra);
     return hipGetLastError();
 }
 

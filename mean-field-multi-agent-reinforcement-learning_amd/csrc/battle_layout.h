@@ -95,6 +95,30 @@ struct State {                      // device pointers; every array is [E][strid
     int32_t* err;                   // [1] sticky device-side error code
 };
 
+// Arguments of the fused rollout step (k_rollout): one launch = one step of the
+// reference training loop (senario_battle.play, :96-171) for every env, with the
+// synthetic rush policy of SURVEY.md 8(d) on device.  All pointers are [E][...] slabs.
+struct RolloutArgs {
+    float* view[kMaxGroups];        // [E][rowcap][VH*VW*NC]   get_observation views
+    float* feat[kMaxGroups];        // [E][rowcap][F]          get_observation features
+    int rowcap;                     // rows per env in every per-agent output (>= max group size)
+    int32_t* actions;               // [E][G][rowcap]  actions taken this step
+    float* rewards;                 // [E][G][rowcap]  get_reward after the step
+    double* mean_act;               // [E][G][n_action] former_act_prob (senario_battle.py:141)
+    float* ep_return;               // [E][G]  running episode return (sum of rewards)
+    int32_t* ep_len;                // [E]     steps into the current episode
+    double* stats;                  // [E][4]  finished episodes, sum final return g0, g1, kills
+    unsigned long long* agent_steps;// [E]     agents present at get_observation, summed
+    const int32_t* tmpl_x;          // [G][tmpl_cap] placement re-applied at each episode start
+    const int32_t* tmpl_y;
+    int tmpl_n[kMaxGroups];
+    int tmpl_cap;
+    int max_steps;                  // episode cap (play(max_steps=400))
+    uint32_t policy_seed;
+    uint32_t step_index;            // global step counter (policy RNG stream)
+    float eps;                      // random-action probability of the rush policy
+};
+
 // meta helpers
 __host__ __device__ inline uint32_t meta_dead(uint32_t m) { return m & 1u; }
 __host__ __device__ inline uint32_t meta_op(uint32_t m) { return (m >> 1) & 3u; }

@@ -40,11 +40,27 @@ class EngineError(RuntimeError):
     pass
 
 
+def _pin_hip_runtime():
+    """PyTorch-ROCm wheels bundle their own HIP/HSA runtime (SONAME libamdhip64.so.7).  If the
+    engine were loaded first it would pull /opt/rocm's runtime into the process, and a later
+    `import torch` would bring a second, conflicting HSA runtime ("No HIP GPUs are available").
+    Importing torch first makes the engine bind to torch's runtime.  MAGENT_PIN_TORCH=0 skips it
+    (processes that never use torch)."""
+    if os.environ.get("MAGENT_PIN_TORCH", "1") == "0":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 class Library:
     """A loaded engine library with checked calls (``lib.env_step(...)`` raises on failure)."""
 
     def __init__(self, path):
         self.path = path
+        if "amd" in os.path.basename(os.path.dirname(os.path.dirname(path))) or path == DEFAULT_LIB:
+            _pin_hip_runtime()
         self._dll = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         for name, argtypes in _SIGS.items():
             fn = getattr(self._dll, name)

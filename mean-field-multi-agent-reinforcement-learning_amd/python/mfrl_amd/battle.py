@@ -1,0 +1,117 @@
+"""BattleBatch: E independent Battle envs resident in HBM (include/magent_amd.h, mfx_battle_*).
+
+The configuration path is the reference's own (magent.GridWorld serialises the config
+through the env_*/gridworld_* ABI); then the env is switched to E instances before its
+first reset.  Two ways to step it:
+
+* per call, on device buffers (``observe / set_action / step / get / clear_dead``) -- the
+  reference call sequence, batched;
+* fused (``rollout_init / rollout_step``) -- one kernel launch per training-loop step
+  (obs x G, on-device rush policy, set_action, step, reward, mean action, clear_dead,
+  episode restart) for all envs: the throughput path measured by bench.py.
+"""
+import ctypes
+
+import numpy as np
+
+import magent
+from magent.gridworld import GridWorld
+
+from . import check, lib
+
+GET_NUM, GET_REWARD, GET_ID, GET_ALIVE, GET_POS, GET_HP = range(6)
+
+
+class BattleBatch:
+    def __init__(self, map_size, n_envs, config="battle", stream=None):
+        L = magent.load_library(lib()._name)
+        self.env = GridWorld(config, map_size=map_size, lib=L) if isinstance(config, str) else GridWorld(config, lib=L)
+        self._dll = L.dll
+        for fn in ("mfx_battle_set_num_envs", "mfx_battle_set_stream", "mfx_battle_observe",
+                   "mfx_battle_set_action", "mfx_battle_step", "mfx_battle_get", "mfx_battle_clear_dead",
+                   "mfx_battle_sync", "mfx_battle_rollout_init", "mfx_battle_rollout_step",
+                   "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
+                   "mfx_battle_group_capacity"):
+            getattr(self._dll, fn).restype = ctypes.c_int
+        self._dll.mfx_last_error.restype = ctypes.c_char_p
+        self.handles = self.env.get_handles()
+        self.n_envs = n_envs
+        self.game = self.env.game
+        self._check(self._dll.mfx_battle_set_num_envs(self.game, n_envs), "set_num_envs")
+        if stream is not None:
+            self.set_stream(stream)
+
+    def _check(self, ret, what):
+        if ret != 0:
+            raise magent.EngineError("%s failed: %s" % (what, self._dll.mfx_last_error().decode()))
+
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream (or a raw hipStream_t as int)."""
+        raw = getattr(stream, "cuda_stream", stream)
+        self._check(self._dll.mfx_battle_set_stream(self.game, ctypes.c_void_p(raw)), "set_stream")
+
+    # ------------------------------------------------------------------ reference call sequence
+    def reset(self):
+        self.env.reset()
+
+    def add_agents(self, group, pos):
+        self.env.add_agents(self.handles[group], method="custom", pos=pos)
+
+    def capacity(self, group):
+        c = ctypes.c_int()
+        self._check(self._dll.mfx_battle_group_capacity(self.game, group, ctypes.byref(c)), "capacity")
+        return c.value
+
+    def observe(self, group, view, feature, rowcap):
+        self._check(self._dll.mfx_battle_observe(self.game, group, ctypes.c_void_p(view.data_ptr()),
+                                                 ctypes.c_void_p(feature.data_ptr()), rowcap), "observe")
+
+    def set_action(self, group, actions, rowcap):
+        self._check(self._dll.mfx_battle_set_action(self.game, group, ctypes.c_void_p(actions.data_ptr()), rowcap),
+                    "set_action")
+
+    def step(self, done=None):
+        ptr = ctypes.c_void_p(done.data_ptr()) if done is not None else ctypes.c_void_p()
+        self._check(self._dll.mfx_battle_step(self.game, ptr), "step")
+
+    def get(self, group, what, out, rowcap):
+        self._check(self._dll.mfx_battle_get(self.game, group, what, ctypes.c_void_p(out.data_ptr()), rowcap), "get")
+
+    def clear_dead(self):
+        self._check(self._dll.mfx_battle_clear_dead(self.game), "clear_dead")
+
+    def sync(self):
+        self._check(self._dll.mfx_battle_sync(self.game), "sync")
+
+    # ------------------------------------------------------------------ fused rollout
+    def rollout_init(self, placement, max_steps=400, eps=0.2, seed=0, stagger=True):
+        """placement: list over groups of [(x, y[, dir]), ...] re-applied at every episode start.
+
+        stagger: spread the episode phase over envs (env e's first episode is cut short by
+        e*max_steps/E steps), so after max_steps steps the batch holds every phase of an episode."""
+        G = len(self.handles)
+        n = (ctypes.c_int * G)(*[len(p) for p in placement])
+        self._keep = [np.ascontiguousarray(np.asarray(p, dtype=np.int32)[:, :2]) for p in placement]
+        xs = [np.ascontiguousarray(a[:, 0]) for a in self._keep]
+        ys = [np.ascontiguousarray(a[:, 1]) for a in self._keep]
+        self._keep += xs + ys
+        P = ctypes.POINTER(ctypes.c_int)
+        px = (P * G)(*[a.ctypes.data_as(P) for a in xs])
+        py = (P * G)(*[a.ctypes.data_as(P) for a in ys])
+        self._check(self._dll.mfx_battle_rollout_init(self.game, n, px, py, max_steps, ctypes.c_float(eps),
+                                                      ctypes.c_uint(seed), int(stagger)),
+                    "rollout_init")
+        rc = ctypes.c_int()
+        self._dll.mfx_battle_rollout_rowcap(self.game, ctypes.byref(rc))
+        self.rowcap = rc.value
+
+    def rollout_step(self, n_steps=1):
+        self._check(self._dll.mfx_battle_rollout_step(self.game, n_steps), "rollout_step")
+
+    def rollout_copy(self, name, dst, group=0, nbytes=None):
+        """Copy a device rollout buffer into dst (numpy array or torch tensor, host or device)."""
+        ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else dst.ctypes.data
+        size = nbytes if nbytes is not None else (dst.numel() * dst.element_size() if hasattr(dst, "numel")
+                                                  else dst.nbytes)
+        self._check(self._dll.mfx_battle_rollout_copy(self.game, name.encode(), group, ctypes.c_void_p(ptr),
+                                                      ctypes.c_size_t(size)), "rollout_copy")

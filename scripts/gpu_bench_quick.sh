@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+for E in 1024 4096; do
+  timeout -k 10 300 python bench.py --steps 50 --warmup 5 --envs $E --no-cpu-baseline > gpurun_out/bench_E$E.json 2> gpurun_out/bench_E$E.err || exit 1
+done

@@ -1,0 +1,81 @@
+"""The fused rollout kernel (k_rollout, bench path) against the C oracle.
+
+Every env of the batch is replayed on the oracle with the actions the on-device policy
+chose; observations (views + features), rewards, mean actions (former_act_prob) and the
+episode restart at max_steps must match bit for bit."""
+import numpy as np
+import pytest
+
+import battle_driver as bd
+import common
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(map_size, n_side, E, T, max_steps):
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    left, right = bd.block_positions(map_size, n_side)
+    eng = BattleBatch(map_size, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=99, stagger=False)
+    rc = eng.rowcap
+    VF, F = 13 * 13 * 7, 34
+    recs = []
+    for t in range(T):
+        eng.rollout_step(1)
+        r = {}
+        for g in range(2):
+            r["view%d" % g] = torch.empty(E * rc * VF, dtype=torch.float32)
+            r["feat%d" % g] = torch.empty(E * rc * F, dtype=torch.float32)
+            eng.rollout_copy("view", r["view%d" % g], group=g)
+            eng.rollout_copy("feature", r["feat%d" % g], group=g)
+        r["act"] = torch.empty(E * 2 * rc, dtype=torch.int32)
+        r["rew"] = torch.empty(E * 2 * rc, dtype=torch.float32)
+        r["mean"] = torch.empty(E * 2 * 21, dtype=torch.float64)
+        eng.rollout_copy("actions", r["act"])
+        eng.rollout_copy("rewards", r["rew"])
+        eng.rollout_copy("mean_action", r["mean"])
+        eng.sync()
+        recs.append({k: v.numpy() for k, v in r.items()})
+    return recs, rc
+
+
+@pytest.mark.parametrize("map_size,n_side,E,T,max_steps", [(24, 18, 3, 45, 20), (64, 128, 2, 70, 400)])
+def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps):
+    recs, rc = _run(map_size, n_side, E, T, max_steps)
+    left, right = bd.block_positions(map_size, n_side)
+    VF, F = 13 * 13 * 7, 34
+    for e in range(E):
+        env, h = common.battle_env(common.ORACLE_LIB, map_size)
+        ep_len = 0
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        for t in range(T):
+            r = recs[t]
+            acts = []
+            for g in range(2):
+                v, f = env.get_observation(h[g])
+                n = len(v)
+                gv = r["view%d" % g].reshape(E, rc, VF)[e, :n]
+                gf = r["feat%d" % g].reshape(E, rc, F)[e, :n]
+                assert gv.tobytes() == v.reshape(n, VF).tobytes(), (e, t, g, "view")
+                assert gf.tobytes() == f.tobytes(), (e, t, g, "feature")
+                a = r["act"].reshape(E, 2, rc)[e, g, :n].astype(np.int32)
+                acts.append(a)
+                mean = np.mean(list(map(lambda x: np.eye(21)[x], a)), axis=0) if n else np.zeros(21)
+                assert r["mean"].reshape(E, 2, 21)[e, g].tobytes() == mean.tobytes(), (e, t, g, "mean")
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rw = env.get_reward(h[g])
+                assert r["rew"].reshape(E, 2, rc)[e, g, :len(rw)].tobytes() == rw.tobytes(), (e, t, g, "reward")
+            env.clear_dead()
+            ep_len += 1
+            if done or ep_len >= max_steps:
+                ep_len = 0
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
+        del env
