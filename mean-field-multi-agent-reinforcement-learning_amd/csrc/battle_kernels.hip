@@ -176,7 +176,10 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
 //  Map.cc:130-218).  Output rows are staged in LDS K agents at a time and streamed out
 //  as 16-byte coalesced stores.
 // ==================================================================================
-constexpr int kObsK = 4;          // agents per staging round (K*1183*4 B = 18.9 KB for Battle)
+#ifndef MFX_OBS_K
+#define MFX_OBS_K 4
+#endif
+constexpr int kObsK = MFX_OBS_K;  // agents per staging round (K*1183*4 B per round for Battle)
 constexpr int kMaxCh = 1 + 3 * kMaxGroups;
 
 struct ObsSmem {                  // LDS carve-up of the observation kernels
@@ -212,7 +215,7 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < G * NV; i += blockDim.x) {
+    for (int i = threadIdx.x; i < G * NV; i += blockDim.x) {   // in place: mm aliases hist
         const int j = i / NV;
         const int n = v.grp_n[j];
         // 0/0 gives the x86 default NaN (0xFFC00000) in the reference; reproduce its bits.
@@ -318,7 +321,7 @@ __host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
 
 __host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int cap) {
     const size_t NV = (size_t)gp.type[g].view_w * gp.type[g].view_h;
-    return (size_t)kObsK * NV * gp.n_ch * 4 + 2 * (((size_t)gp.n_groups * NV * 4 + 15) & ~(size_t)15) +
+    return (size_t)kObsK * NV * gp.n_ch * 4 + (((size_t)gp.n_groups * NV * 4 + 15) & ~(size_t)15) +
            (((size_t)cap * 2 + 15) & ~(size_t)15) + 16 + ((NV + 15) & ~(size_t)15);
 }
 
@@ -328,7 +331,7 @@ __device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, i
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     ObsSmem sm;
     sm.stage = reinterpret_cast<float*>(smem + off); off += (size_t)kObsK * NV * gp.n_ch * 4;
-    sm.mm = reinterpret_cast<float*>(smem + off);    off += r16(G * NV * 4);
+    sm.mm = reinterpret_cast<float*>(smem + off);    // the histogram is converted in place
     sm.hist = reinterpret_cast<int*>(smem + off);    off += r16(G * NV * 4);
     sm.bin = reinterpret_cast<uint16_t*>(smem + off); off += r16((size_t)cap * 2);
     sm.type_hp = reinterpret_cast<float*>(smem + off); off += 16;
@@ -428,12 +431,38 @@ __global__ void __launch_bounds__(256) k_set_action(const GameParams* __restrict
 // ==================================================================================
 //  step (GridWorld.cc:498-694)
 // ==================================================================================
+struct SerialType {          // what the one-lane loops read per group, kept in LDS (the group
+    float hp, damage, kill_supply, kill_reward, dead_penalty, attack_penalty;   // index is
+    int attack_in_group, att_x_off, att_y_off, pad;                              // lane-varying:
+    int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];                       // from global it
+    int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];                     // would be a vector
+};                                                                               // load per use)
+
 struct StepSmem {
     int wave_tot[16];
     int flags[8];       // [0..kMaxRules) rule triggers
+    SerialType tt[kMaxGroups];
 };
 
-__device__ __forceinline__ void do_attack_serial(const GameParams& gp, EnvView& v, uint32_t* atk, int n_atk) {
+__device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem& sm) {
+    for (int g = 0; g < gp.n_groups; ++g) {
+        const TypeParams& T = gp.type[g];
+        SerialType& S = sm.tt[g];
+        const int t = threadIdx.x;
+        if (t < kMaxRangeCount) {
+            S.att_dx[t] = T.att_dx[t]; S.att_dy[t] = T.att_dy[t];
+            S.move_dx[t] = T.move_dx[t]; S.move_dy[t] = T.move_dy[t];
+        }
+        if (t == 0) {
+            S.hp = T.hp; S.damage = T.damage; S.kill_supply = T.kill_supply; S.kill_reward = T.kill_reward;
+            S.dead_penalty = T.dead_penalty; S.attack_penalty = T.attack_penalty;
+            S.attack_in_group = T.attack_in_group; S.att_x_off = T.att_x_off; S.att_y_off = T.att_y_off;
+        }
+    }
+}
+
+__device__ __forceinline__ void do_attack_serial(const GameParams& gp, const StepSmem& sm, EnvView& v, uint32_t* atk,
+                                                 int n_atk) {
     // shuffled order, strictly sequential (the reference loop is racy with OMP>1; OMP=1 semantics)
     const int W = gp.W, H = gp.H;
     for (int i = 0; i < n_atk; ++i) {
@@ -442,7 +471,7 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, EnvView& 
         uint32_t m = v.meta[id];
         if (meta_dead(m)) continue;
         const int g = meta_group(m);
-        const TypeParams& T = gp.type[g];
+        const SerialType& T = sm.tt[g];
         const uint32_t p = v.xy[id];
         const int ox = (int)(p & 0xFFFF) + T.att_x_off + T.att_dx[ai];
         const int oy = (int)(p >> 16) + T.att_y_off + T.att_dy[ai];
@@ -452,7 +481,7 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, EnvView& 
         const uint32_t om = v.meta[cv];
         const int og = meta_group(om);
         if (!T.attack_in_group && og == g) { v.next_r[id] += T.attack_penalty; continue; }
-        const TypeParams& OT = gp.type[og];
+        const SerialType& OT = sm.tt[og];
         float reward = 0.0f;
         const float ohp = v.hp[cv] - T.damage;                                    // Agent::be_attack
         v.hp[cv] = ohp;
@@ -475,13 +504,13 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, EnvView& 
     }
 }
 
-__device__ __forceinline__ void do_move_one(const GameParams& gp, EnvView& v, uint32_t ent) {
+__device__ __forceinline__ void do_move_one(const GameParams& gp, const StepSmem& sm, EnvView& v, uint32_t ent) {
     // GridWorld.cc:631-660 + Map::do_move (Map.cc:324-369), NORTH, 1x1
     const int id = (int)(ent >> 16), mi = (int)((ent >> 8) & 0xFF);
     const uint32_t m = v.meta[id];
     if (meta_dead(m)) return;
     const int W = gp.W, H = gp.H;
-    const TypeParams& T = gp.type[meta_group(m)];
+    const SerialType& T = sm.tt[meta_group(m)];
     const uint32_t p = v.xy[id];
     const int x = p & 0xFFFF, y = p >> 16;
     const int nx = x + T.move_dx[mi], ny = y + T.move_dy[mi];
@@ -503,6 +532,8 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
                          uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
                          int& done_out) {
     const int G = gp.n_groups;
+    load_serial_types(gp, sm);
+    __syncthreads();
     // ---- shuffle + attack: one lane (GridWorld.cc:507-558)
     if (threadIdx.x == 0) {
         uint32_t x = rng;
@@ -512,7 +543,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
             const uint32_t t = atk[i]; atk[i] = atk[j]; atk[j] = t;
         }
         rng = x;
-        do_attack_serial(gp, v, atk, n_atk);
+        do_attack_serial(gp, sm, v, atk, n_atk);
     }
     __syncthreads();
     // ---- starve (GridWorld.cc:570-595): independent per agent
@@ -560,7 +591,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
         order = sorted;
     }
     if (threadIdx.x == 0)
-        for (int i = 0; i < n_mov; ++i) do_move_one(gp, v, order[i]);
+        for (int i = 0; i < n_mov; ++i) do_move_one(gp, sm, v, order[i]);
     __syncthreads();
     // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
     for (int r = 0; r < gp.n_rules; ++r) {
@@ -769,23 +800,55 @@ __device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-o
     return r;
 }
 
+// LDS plan of k_rollout: the env (cells, per-id arrays, group lists) + the observation scratch.
+// The staging buffer of the observation rounds is dead once the last row is streamed out, so the
+// policy actions, action histogram, attack/move buffers and the reduction area reuse it.
+struct RolloutUnion { size_t act, ahist, atk, mov, sorted, red, total; };
+
+__host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int cap, int acap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    RolloutUnion u;
+    size_t o = 0;
+    u.act = o;    o += r16((size_t)gp.n_groups * cap * 4);
+    u.ahist = o;  o += r16((size_t)gp.n_groups * 64 * 4);
+    u.atk = o;    o += r16((size_t)acap * 4);
+    u.mov = o;    o += r16((size_t)acap * 4);
+    u.sorted = o; o += gp.large_map ? r16((size_t)acap * 4) : 0;
+    u.red = o;    o += r16(1024 * 4);                  // block_sum scratch, up to 1024 threads
+    u.total = o;
+    return u;
+}
+
 size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const int G = gp.n_groups;
+    const size_t NV = (size_t)gp.type[0].view_w * gp.type[0].view_h;
+    const size_t stage = (size_t)kObsK * NV * gp.n_ch * 4;
     size_t b = r16((size_t)cells_n * 2);
     b += 6 * r16((size_t)cap * 4) + r16(cap);             // xy hp next_r last_r last_act op_obj + meta
-    b += r16((size_t)G * cap * 4) * 2;                     // grp_ids + policy actions
-    b += 3 * r16((size_t)acap * 4);                        // atk mov sorted
-    b += 4 * r16(G * 4) + r16(256 * 4) + r16((size_t)G * 64 * 4);   // counts, reduction, action histogram
-    b += obs_smem_core(gp, 0, cap);
+    b += r16((size_t)G * cap * 4);                         // grp_ids
+    b += 4 * r16(G * 4);                                   // grp_n grp_dead grp_reward n_before
+    b += obs_smem_core(gp, 0, cap);                        // includes the staging buffer
+    const RolloutUnion u = rollout_union(gp, cap, acap);
+    if (u.total > stage) b += r16(u.total - stage);
     return b;
 }
 
+__device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes) {   // 16-B aligned, bytes % 16 == 0
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const uint4* q = reinterpret_cast<const uint4*>(src);
+    for (size_t i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = q[i];
+}
+
+#ifndef MFX_ROLLOUT_THREADS
+#define MFX_ROLLOUT_THREADS 256
+#endif
 template <bool kB>
-__global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ gpp, State s, RolloutArgs ra) {
+__global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParams* __restrict__ gpp, State s, RolloutArgs ra) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ StepSmem sm;
-    __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 2 id_counter, 3 done
+    __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 2 id_counter, 3 episode end, 4 old id_counter
+    __shared__ unsigned long long steps_acc;
     const GameParams& gp = *gpp;
     const int e = blockIdx.x, G = gp.n_groups, cap = s.cap, acap = s.acap;
     EnvView gv = global_view(s, e, G);
@@ -803,46 +866,45 @@ __global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ 
     v.op_obj = reinterpret_cast<int32_t*>(carve((size_t)cap * 4));
     v.meta = reinterpret_cast<uint8_t*>(carve((size_t)cap));
     v.grp_ids = reinterpret_cast<int32_t*>(carve((size_t)G * cap * 4));
-    int32_t* act = reinterpret_cast<int32_t*>(carve((size_t)G * cap * 4));
-    uint32_t* atk = reinterpret_cast<uint32_t*>(carve((size_t)acap * 4));
-    uint32_t* mov = reinterpret_cast<uint32_t*>(carve((size_t)acap * 4));
-    uint32_t* sorted = reinterpret_cast<uint32_t*>(carve((size_t)acap * 4));
     v.grp_n = reinterpret_cast<int32_t*>(carve(G * 4));
     v.grp_dead = reinterpret_cast<int32_t*>(carve(G * 4));
     v.grp_reward = reinterpret_cast<float*>(carve(G * 4));
     int32_t* n_before = reinterpret_cast<int32_t*>(carve(G * 4));
-    float* red = reinterpret_cast<float*>(carve(256 * 4));
-    int* ahist = reinterpret_cast<int*>(carve((size_t)G * 64 * 4));
     ObsSmem osm = carve_obs(smem, gp, 0, cap, off);
+    const RolloutUnion u = rollout_union(gp, cap, acap);
+    char* uni = reinterpret_cast<char*>(osm.stage);
+    int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
+    int* ahist = reinterpret_cast<int*>(uni + u.ahist);
+    uint32_t* atk = reinterpret_cast<uint32_t*>(uni + u.atk);
+    uint32_t* mov = reinterpret_cast<uint32_t*>(uni + u.mov);
+    uint32_t* sorted = reinterpret_cast<uint32_t*>(uni + u.sorted);
+    float* red = reinterpret_cast<float*>(uni + u.red);
     MFX_STAMP(0);
-    // ---------------- load the env
-    const int nid = s.id_counter[e];
-    if ((s.cells_n & 7) == 0) {   // per-env slab is 16-B aligned: move 8 cells per lane
-        for (int i = threadIdx.x; i < (s.cells_n >> 3); i += blockDim.x)
-            reinterpret_cast<uint4*>(v.cells)[i] = reinterpret_cast<const uint4*>(gv.cells)[i];
-    } else if ((s.cells_n & 1) == 0) {
-        for (int i = threadIdx.x; i < (s.cells_n >> 1); i += blockDim.x)
-            reinterpret_cast<uint32_t*>(v.cells)[i] = reinterpret_cast<const uint32_t*>(gv.cells)[i];
+    // ---------------- load the env (whole 16-B rows; cap is a power of two >= 64)
+    if ((s.cells_n & 7) == 0) {
+        copy16(v.cells, gv.cells, (size_t)s.cells_n * 2);
     } else {
         for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
     }
-    for (int i = threadIdx.x; i < nid; i += blockDim.x) {
-        v.xy[i] = gv.xy[i]; v.hp[i] = gv.hp[i]; v.next_r[i] = gv.next_r[i]; v.last_r[i] = gv.last_r[i];
-        v.last_act[i] = gv.last_act[i]; v.op_obj[i] = gv.op_obj[i]; v.meta[i] = gv.meta[i];
-    }
+    copy16(v.xy, gv.xy, (size_t)cap * 4);
+    copy16(v.hp, gv.hp, (size_t)cap * 4);
+    copy16(v.next_r, gv.next_r, (size_t)cap * 4);
+    copy16(v.last_r, gv.last_r, (size_t)cap * 4);
+    copy16(v.last_act, gv.last_act, (size_t)cap * 4);
+    copy16(v.op_obj, gv.op_obj, (size_t)cap * 4);
+    copy16(v.meta, gv.meta, (size_t)cap);
+    copy16(v.grp_ids, gv.grp_ids, (size_t)G * cap * 4);
     if (threadIdx.x < G) {
-        v.grp_n[threadIdx.x] = gv.grp_n[threadIdx.x];
+        const int n = gv.grp_n[threadIdx.x];
+        v.grp_n[threadIdx.x] = n;
+        n_before[threadIdx.x] = n;
         v.grp_dead[threadIdx.x] = gv.grp_dead[threadIdx.x];
         v.grp_reward[threadIdx.x] = gv.grp_reward[threadIdx.x];
     }
-    __syncthreads();
-    for (int g = 0; g < G; ++g)
-        for (int i = threadIdx.x; i < v.grp_n[g]; i += blockDim.x) v.grp_ids[g * cap + i] = gv.grp_ids[g * cap + i];
     if (threadIdx.x == 0) {
         misc[0] = 0; misc[1] = 0;
-        unsigned long long tot = 0;
-        for (int g = 0; g < G; ++g) { n_before[g] = v.grp_n[g]; tot += (unsigned)v.grp_n[g]; }
-        ra.agent_steps[e] += tot;
+        misc[4] = s.id_counter[e];
+        steps_acc = ra.agent_steps[e];
     }
     __syncthreads();
     MFX_STAMP(1);
@@ -860,12 +922,15 @@ __global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ 
         for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
     }
     MFX_STAMP(3);
-    // ---------------- policy + mean action (former_act_prob)
-    for (int g = 0; g < G; ++g) {
-        const int n = v.grp_n[g], na = gp.type[g].n_action;
-        for (int i = threadIdx.x; i < 64; i += blockDim.x) ahist[g * 64 + i] = 0;
+    // ---------------- policy + mean action (former_act_prob), all groups in one pass
+    {
+        int ntot = 0;
+        for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+        for (int i = threadIdx.x; i < G * 64; i += blockDim.x) ahist[i] = 0;
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        for (int t = threadIdx.x; t < ntot; t += blockDim.x) {
+            int g = 0, i = t;
+            while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
             const int id = v.grp_ids[g * cap + i];
             const uint32_t key = ra.policy_seed ^ mix32(ra.step_index * 0x9E3779B9u + (uint32_t)e * 0x632BE5ABu) ^
                                  mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
@@ -875,8 +940,10 @@ __global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ 
             atomicAdd(&ahist[g * 64 + a], 1);
         }
         __syncthreads();
-        for (int k = threadIdx.x; k < na; k += blockDim.x)
-            ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[g * 64 + k] / (double)n : 0.0;
+        for (int t = threadIdx.x; t < G * 64; t += blockDim.x) {
+            const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
+            if (k < na) ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : 0.0;
+        }
     }
     MFX_STAMP(4);
     // ---------------- set_action (group order) and step
@@ -923,7 +990,7 @@ __global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ 
         s.done[e] = done;
     }
     __syncthreads();
-    int id_counter = nid;
+    int id_counter = misc[4];
     if (misc[3]) {
         const int W = gp.W, H = gp.H;
         for (int c = threadIdx.x; c < W * H; c += blockDim.x) {
@@ -956,26 +1023,33 @@ __global__ void __launch_bounds__(256) k_rollout(const GameParams* __restrict__ 
     MFX_STAMP(9);
     // ---------------- write the env back
     if ((s.cells_n & 7) == 0) {
-        for (int i = threadIdx.x; i < (s.cells_n >> 3); i += blockDim.x)
-            reinterpret_cast<uint4*>(gv.cells)[i] = reinterpret_cast<const uint4*>(v.cells)[i];
-    } else if ((s.cells_n & 1) == 0) {
-        for (int i = threadIdx.x; i < (s.cells_n >> 1); i += blockDim.x)
-            reinterpret_cast<uint32_t*>(gv.cells)[i] = reinterpret_cast<const uint32_t*>(v.cells)[i];
+        copy16(gv.cells, v.cells, (size_t)s.cells_n * 2);
     } else {
         for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
     }
-    for (int i = threadIdx.x; i < id_counter; i += blockDim.x) {
-        gv.xy[i] = v.xy[i]; gv.hp[i] = v.hp[i]; gv.next_r[i] = v.next_r[i]; gv.last_r[i] = v.last_r[i];
-        gv.last_act[i] = v.last_act[i]; gv.op_obj[i] = v.op_obj[i]; gv.meta[i] = v.meta[i];
+    {
+        const size_t n4 = ((size_t)id_counter + 3) & ~(size_t)3, n16 = ((size_t)id_counter + 15) & ~(size_t)15;
+        copy16(gv.xy, v.xy, n4 * 4);
+        copy16(gv.hp, v.hp, n4 * 4);
+        copy16(gv.next_r, v.next_r, n4 * 4);
+        copy16(gv.last_r, v.last_r, n4 * 4);
+        copy16(gv.last_act, v.last_act, n4 * 4);
+        copy16(gv.op_obj, v.op_obj, n4 * 4);
+        copy16(gv.meta, v.meta, n16);
+        for (int g = 0; g < G; ++g)
+            copy16(gv.grp_ids + g * cap, v.grp_ids + g * cap, (((size_t)v.grp_n[g] + 3) & ~(size_t)3) * 4);
     }
-    for (int g = 0; g < G; ++g)
-        for (int i = threadIdx.x; i < v.grp_n[g]; i += blockDim.x) gv.grp_ids[g * cap + i] = v.grp_ids[g * cap + i];
     if (threadIdx.x < G) {
         gv.grp_n[threadIdx.x] = v.grp_n[threadIdx.x];
         gv.grp_dead[threadIdx.x] = v.grp_dead[threadIdx.x];
         gv.grp_reward[threadIdx.x] = v.grp_reward[threadIdx.x];
     }
-    if (threadIdx.x == 0) { s.id_counter[e] = id_counter; s.n_atk[e] = 0; s.n_mov[e] = 0; }
+    if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int g = 0; g < G; ++g) tot += (unsigned)n_before[g];
+        ra.agent_steps[e] = steps_acc + tot;
+        s.id_counter[e] = id_counter; s.n_atk[e] = 0; s.n_mov[e] = 0;
+    }
     MFX_STAMP(10);
 }
 
@@ -1053,9 +1127,9 @@ hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const St
     const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     if (is_battle_shape(gp))
-        k_rollout<true><<<s.E, 256, smem, st>>>(d_gp, s, ra);
+        k_rollout<true><<<s.E, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, s, ra);
     else
-        k_rollout<false><<<s.E, 256, smem, st>>>(d_gp, s, ra);
+        k_rollout<false><<<s.E, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, s, ra);
     return hipGetLastError();
 }
 
