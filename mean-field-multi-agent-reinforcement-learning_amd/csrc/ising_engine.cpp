@@ -1,0 +1,135 @@
+// ising_engine.cpp -- host runtime + C ABI of the Ising lattice and tabular MF-Q kernels.
+//
+// The reference has no native layer here (everything is python: examples/ising_model and
+// main_MFQ_Ising.py).  This ABI is what this repository's drop-in `examples.ising_model`
+// package and `mfrl_amd.ising` bind through ctypes; host buffers in, host buffers out.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "ising_kernels.h"
+#include "mfx_common.h"
+
+namespace mfx {
+
+struct IsingEngine {
+    int R = 1, N = 0, K = 0;
+    hipStream_t stream = nullptr;
+    DevBuf<int16_t> nbr;
+    DevBuf<uint8_t> spins, obs, spins_out;
+    DevBuf<int32_t> actions, n_up, steps;
+    DevBuf<double> reward, order, q, u, order_t;
+    DevBuf<uint32_t> mask;
+    DevBuf<int32_t> nup_t;
+    ~IsingEngine() { if (stream) (void)hipStreamDestroy(stream); }
+};
+
+}  // namespace mfx
+
+using mfx::IsingEngine;
+
+extern "C" {
+
+// R replicas of an N-agent lattice whose neighbour table nbr[N][K] (ascending ids) comes from
+// Ising.py:_calc_mask (computed by the python Scenario).
+MFX_API int mfx_ising_create(int R, int N, int K, const int16_t* nbr, void** handle) {
+    if (R < 1 || N < 1 || N > 1024 || K < 1 || K > 16) return mfx::fail("ising: need 1 <= N <= 1024, 1 <= K <= 16");
+    try {
+        auto* e = new IsingEngine();
+        e->R = R; e->N = N; e->K = K;
+        MFX_HIP_THROW(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        e->nbr.ensure((size_t)N * K);
+        MFX_HIP_THROW(hipMemcpy(e->nbr.p, nbr, sizeof(int16_t) * N * K, hipMemcpyHostToDevice));
+        e->spins.ensure((size_t)R * N);
+        MFX_HIP_THROW(hipMemset(e->spins.p, 0, (size_t)R * N));
+        *handle = e;
+        return 0;
+    } catch (const std::exception& ex) {
+        return mfx::fail("%s", ex.what());
+    }
+}
+
+MFX_API int mfx_ising_destroy(void* h) { delete static_cast<IsingEngine*>(h); return 0; }
+
+MFX_API int mfx_ising_set_spins(void* h, const uint8_t* spins) {
+    auto* e = static_cast<IsingEngine*>(h);
+    MFX_HIP(hipMemcpy(e->spins.p, spins, (size_t)e->R * e->N, hipMemcpyHostToDevice));
+    return 0;
+}
+
+MFX_API int mfx_ising_get_spins(void* h, uint8_t* spins) {
+    auto* e = static_cast<IsingEngine*>(h);
+    MFX_HIP(hipMemcpy(spins, e->spins.p, (size_t)e->R * e->N, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// One IsingMultiAgentEnv.step for every replica: actions [R][N] -> rewards [R][N] f64,
+// observations [R][N][K] u8 (neighbour spins), n_up [R], order parameter [R].
+MFX_API int mfx_ising_step(void* h, const int32_t* actions, double* reward, uint8_t* obs, int32_t* n_up,
+                           double* order) {
+    auto* e = static_cast<IsingEngine*>(h);
+    const size_t RN = (size_t)e->R * e->N;
+    try {
+        e->actions.ensure(RN); e->reward.ensure(RN); e->obs.ensure(RN * e->K); e->n_up.ensure(e->R);
+        e->order.ensure(e->R);
+    } catch (const std::exception& ex) {
+        return mfx::fail("%s", ex.what());
+    }
+    MFX_HIP(hipMemcpyAsync(e->actions.p, actions, sizeof(int32_t) * RN, hipMemcpyHostToDevice, e->stream));
+    MFX_HIP(mfx::launch_ising_step(e->R, e->N, e->K, e->nbr.p, e->spins.p, e->actions.p, e->reward.p, e->obs.p,
+                                   e->n_up.p, e->order.p, e->stream));
+    MFX_HIP(hipMemcpyAsync(reward, e->reward.p, sizeof(double) * RN, hipMemcpyDeviceToHost, e->stream));
+    MFX_HIP(hipMemcpyAsync(obs, e->obs.p, RN * e->K, hipMemcpyDeviceToHost, e->stream));
+    MFX_HIP(hipMemcpyAsync(n_up, e->n_up.p, sizeof(int32_t) * e->R, hipMemcpyDeviceToHost, e->stream));
+    MFX_HIP(hipMemcpyAsync(order, e->order.p, sizeof(double) * e->R, hipMemcpyDeviceToHost, e->stream));
+    MFX_HIP(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// The whole tabular MF-Q episode of main_MFQ_Ising.py for every replica, starting from the
+// current spins.  u: host [R][T][N] uniforms or null (Philox, `seed`); mask: host
+// [R][T][ceil(N/32)] act_group bits or null (act_rate 1).  Outputs (host, nullable except q):
+// q [R][N][K+1][2], order [R][T], n_up [R][T], steps [R]; spins are updated in place.
+MFX_API int mfx_ising_mfq_run(void* h, int T, double temperature, double lr, double decay_rate, int decay_gap,
+                              const double* u, const uint32_t* mask, unsigned seed, double* q, double* order,
+                              int32_t* n_up, int32_t* steps) {
+    auto* e = static_cast<IsingEngine*>(h);
+    const int R = e->R, N = e->N, K = e->K, words = (N + 31) / 32;
+    if (T < 1) return mfx::fail("ising mfq: T must be >= 1");
+    if (decay_gap < 1) return mfx::fail("ising mfq: decay_gap must be >= 1");
+    mfx::IsingMfqArgs a{};
+    try {
+        if (u) {
+            e->u.ensure((size_t)R * T * N);
+            MFX_HIP_THROW(hipMemcpyAsync(e->u.p, u, sizeof(double) * R * T * N, hipMemcpyHostToDevice, e->stream));
+        }
+        if (mask) {
+            e->mask.ensure((size_t)R * T * words);
+            MFX_HIP_THROW(hipMemcpyAsync(e->mask.p, mask, sizeof(uint32_t) * R * T * words, hipMemcpyHostToDevice,
+                                         e->stream));
+        }
+        e->q.ensure((size_t)R * N * (K + 1) * 2);
+        e->order_t.ensure((size_t)R * T);
+        e->nup_t.ensure((size_t)R * T);
+        e->steps.ensure(R);
+        e->spins_out.ensure((size_t)R * N);
+    } catch (const std::exception& ex) {
+        return mfx::fail("%s", ex.what());
+    }
+    a.N = N; a.K = K; a.T = T; a.nbr = e->nbr.p; a.spins0 = e->spins.p;
+    a.u = u ? e->u.p : nullptr; a.mask = mask ? e->mask.p : nullptr;
+    a.temperature = temperature; a.lr = lr; a.decay_rate = decay_rate; a.decay_gap = decay_gap; a.seed = seed;
+    a.q_out = e->q.p; a.order_out = e->order_t.p; a.nup_out = e->nup_t.p; a.spins_out = e->spins_out.p;
+    a.steps_out = e->steps.p;
+    MFX_HIP(mfx::launch_ising_mfq(a, R, e->stream));
+    MFX_HIP(hipMemcpyAsync(e->spins.p, e->spins_out.p, (size_t)R * N, hipMemcpyDeviceToDevice, e->stream));
+    MFX_HIP(hipMemcpyAsync(q, e->q.p, sizeof(double) * R * N * (K + 1) * 2, hipMemcpyDeviceToHost, e->stream));
+    if (order) MFX_HIP(hipMemcpyAsync(order, e->order_t.p, sizeof(double) * R * T, hipMemcpyDeviceToHost, e->stream));
+    if (n_up) MFX_HIP(hipMemcpyAsync(n_up, e->nup_t.p, sizeof(int32_t) * R * T, hipMemcpyDeviceToHost, e->stream));
+    if (steps) MFX_HIP(hipMemcpyAsync(steps, e->steps.p, sizeof(int32_t) * R, hipMemcpyDeviceToHost, e->stream));
+    MFX_HIP(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,188 @@
+// ising_kernels.hip -- Ising spin lattice + tabular mean-field Q-learning on gfx950.
+//
+// Reference: examples/ising_model/Ising.py (_calc_mask :7-58, reset :79-99, reward :101-111,
+// observation :113-119), multiagent/core.py (IsingWorld.step :99-125) and the MF-Q loop of
+// main_MFQ_Ising.py (:55-67 Boltzmann exploration, :103-159 episode loop).
+//
+// Layout: R independent replicas of an L x L periodic lattice, N = L*L agents, agent i at
+// row i / L, column i % L (Ising.py:81-90).  One workgroup per replica, one thread per spin.
+//   spins  u8  [R][N]        0 = down, 1 = up (global_state)
+//   nbr    i16 [N][K]        neighbour ids of agent i in ascending id order (spin_mask == 1)
+//   Q      f64 [R][N][K+1][2]
+// All float64 arithmetic is the reference's own sequence of single IEEE operations
+// (-ffp-contract=off).  exp() is the device libm; see DESIGN.md for why an ulp there cannot
+// change an action in practice.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "ising_kernels.h"
+
+namespace mfx {
+
+constexpr int kIsingMaxK = 16;
+
+// ------------------------------------------------------------------ env step
+// IsingMultiAgentEnv._step (environment.py:49-78): spin_i := action_i for every agent, then
+// n_up / order parameter (core.py:110-116), then per agent observation (neighbour spins) and
+// reward 0.5 * s_i * sum_j s_j in +-1 units (Ising.py:101-111), all on the NEW spins.
+__global__ void __launch_bounds__(1024) k_ising_step(int N, int K, const int16_t* __restrict__ nbr,
+                                                     uint8_t* __restrict__ spins, const int32_t* __restrict__ actions,
+                                                     double* __restrict__ reward, uint8_t* __restrict__ obs,
+                                                     int32_t* __restrict__ n_up, double* __restrict__ order) {
+    __shared__ uint8_t sp[4096];
+    __shared__ int cnt;
+    const int r = blockIdx.x;
+    uint8_t* S = spins + (size_t)r * N;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    int mine = 0;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const uint8_t s = actions[(size_t)r * N + i] <= 0 ? 0 : 1;       // _set_action (:112-114)
+        sp[i] = s;
+        S[i] = s;
+        mine += s;
+    }
+    atomicAdd(&cnt, mine);
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        int sum = 0;
+        for (int k = 0; k < K; ++k) {
+            const int j = nbr[i * K + k];
+            obs[((size_t)r * N + i) * K + k] = sp[j];
+            sum += sp[j] ? 1 : -1;
+        }
+        const double gi = sp[i] ? 1.0 : -1.0;
+        const double local = (-0.5 * gi) * (double)sum;               // Ising.py:106-108
+        reward[(size_t)r * N + i] = -local;
+    }
+    if (threadIdx.x == 0) {
+        n_up[r] = cnt;
+        const int down = N - cnt;
+        order[r] = (double)(cnt > down ? cnt - down : down - cnt) / ((double)N + 0.0);
+    }
+}
+
+// ------------------------------------------------------------------ Philox 4x32-10 (perf mode)
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+
+__device__ __forceinline__ double philox_uniform(uint32_t seed, uint32_t rep, uint32_t t, uint32_t i) {
+    uint32_t c[4] = {i, t, rep, 0x5EED1u};
+    philox(c, seed, 0xA511E9B3u);
+    const uint64_t bits = ((uint64_t)(c[0] >> 5) << 26) | (c[1] >> 6);   // 53 bits, like random_sample
+    return (double)bits * (1.0 / 9007199254740992.0);
+}
+
+// ------------------------------------------------------------------ fused MF-Q episode
+// One workgroup = one replica = one run of main_MFQ_Ising.py's episode loop.  Thread i owns agent
+// i's Q rows in registers.  u: [T][N] uniforms per replica step (host-generated from numpy's
+// RandomState for bit parity, or null = Philox); mask: [T][ceil(N/32)] act_group bits (null = all).
+template <int KMAX>
+__global__ void __launch_bounds__(1024) k_ising_mfq(IsingMfqArgs a) {
+    __shared__ uint8_t sp[4096];
+    __shared__ int cnt[2];
+    const int r = blockIdx.x, N = a.N, K = a.K, i = threadIdx.x;
+    const bool own = i < N;
+    double q[KMAX + 1][2];
+#pragma unroll
+    for (int s = 0; s < KMAX + 1; ++s) { q[s][0] = 0.0; q[s][1] = 0.0; }
+    int16_t nb[KMAX];
+    for (int k = 0; k < K; ++k) nb[k] = own ? a.nbr[i * K + k] : 0;
+    if (own) sp[i] = a.spins0[(size_t)r * N + i];
+    if (i == 0) { cnt[0] = 0; cnt[1] = 0; }
+    __syncthreads();
+    double current_t = 0.3, max_order = 0.0;
+    int done_ = 0, t = 0;
+    const int words = (N + 31) >> 5;
+    for (t = 0; t < a.T; ++t) {
+        if (t % a.decay_gap == 0) current_t *= a.decay_rate;           // main_MFQ_Ising.py:108-112
+        if (current_t < a.temperature) current_t = a.temperature;
+        // ---- state = number of up neighbours (count_nonzero(obs == 1)), Boltzmann action (:55-67)
+        int st = 0;
+        int act = 0;
+        if (own) {
+            for (int k = 0; k < K; ++k) st += sp[nb[k]];
+            double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+            for (int s = 0; s < KMAX + 1; ++s) if (s == st) { q0 = q[s][0]; q1 = q[s][1]; }
+            const double e0 = exp(q0 / current_t), e1 = exp(q1 / current_t);
+            const double denom = e0 + e1;
+            const double p0 = e0 / denom, p1 = e1 / denom;
+            const double c0 = p0 / (p0 + p1);                          // cdf /= cdf[-1]
+            const double u = a.u ? a.u[((size_t)r * a.T + t) * N + i]
+                                 : philox_uniform(a.seed, (uint32_t)r, (uint32_t)t, (uint32_t)i);
+            act = (u >= c0) ? 1 : 0;                                   // searchsorted(side='right')
+        }
+        __syncthreads();                                               // every state read the old spins
+        if (own) sp[i] = (uint8_t)act;
+        if (i == 0) cnt[t & 1] = 0;
+        __syncthreads();
+        // ---- world.step: order parameter; reward on the new spins; Q update (:122-133)
+        const int par = t & 1;
+        if (own) {
+            int sum = 0;
+            for (int k = 0; k < K; ++k) sum += sp[nb[k]] ? 1 : -1;
+            const double gi = act ? 1.0 : -1.0;
+            const double rew = -((-0.5 * gi) * (double)sum);
+            const bool upd = !a.mask || ((a.mask[((size_t)r * a.T + t) * words + (i >> 5)] >> (i & 31)) & 1u);
+            if (upd) {
+#pragma unroll
+                for (int s = 0; s < KMAX + 1; ++s)
+                    if (s == st) {
+                        if (act) q[s][1] = q[s][1] + a.lr * (rew - q[s][1]);
+                        else q[s][0] = q[s][0] + a.lr * (rew - q[s][0]);
+                    }
+            }
+        }
+        const unsigned long long up = __ballot(own && act);
+        if ((i & 63) == 0) atomicAdd(&cnt[par], __popcll(up));
+        __syncthreads();
+        const int n_up = cnt[par], n_down = N - n_up;
+        const double order = (double)(n_up > n_down ? n_up - n_down : n_down - n_up) / ((double)N + 0.0);
+        if (i == 0) {
+            if (a.order_out) a.order_out[(size_t)r * a.T + t] = order;
+            if (a.nup_out) a.nup_out[(size_t)r * a.T + t] = n_up;
+        }
+        if (order > max_order) max_order = order;                      // :138-156 (same on all lanes)
+        if (fabs(max_order - order) < 0.001) ++done_;
+        else done_ = 0;
+        if (done_ == 500 || t > a.T) { ++t; break; }
+    }
+    if (own) {
+        double* Q = a.q_out + ((size_t)r * N + i) * (K + 1) * 2;
+        for (int s = 0; s <= K; ++s) {
+#pragma unroll
+            for (int ss = 0; ss < KMAX + 1; ++ss)
+                if (ss == s) { Q[2 * s] = q[ss][0]; Q[2 * s + 1] = q[ss][1]; }
+        }
+        if (a.spins_out) a.spins_out[(size_t)r * N + i] = sp[i];
+    }
+    if (i == 0 && a.steps_out) a.steps_out[r] = t;
+}
+
+hipError_t launch_ising_step(int R, int N, int K, const int16_t* nbr, uint8_t* spins, const int32_t* actions,
+                             double* reward, uint8_t* obs, int32_t* n_up, double* order, hipStream_t st) {
+    if (N > 4096 || K > kIsingMaxK) return hipErrorInvalidValue;
+    const int threads = N >= 1024 ? 1024 : ((N + 63) / 64) * 64;
+    k_ising_step<<<R, threads, 0, st>>>(N, K, nbr, spins, actions, reward, obs, n_up, order);
+    return hipGetLastError();
+}
+
+hipError_t launch_ising_mfq(const IsingMfqArgs& a, int R, hipStream_t st) {
+    if (a.N > 1024 || a.K > kIsingMaxK) return hipErrorInvalidValue;
+    const int threads = ((a.N + 63) / 64) * 64;
+    if (a.K <= 4)
+        k_ising_mfq<4><<<R, threads, 0, st>>>(a);
+    else
+        k_ising_mfq<kIsingMaxK><<<R, threads, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+}  // namespace mfx

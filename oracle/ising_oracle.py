@@ -1,0 +1,77 @@
+"""TEST ORACLE ONLY -- numpy restatement of the Ising MF-Q path (tests/, smoke() and bench.py's
+cpu_baseline leg may use it; the product never does).
+
+Restates, in vectorised numpy of its own:
+  * Ising.py:_calc_mask (:7-58)               -> neighbours()
+  * IsingWorld.step + Scenario.reward/observation (core.py:99-125, Ising.py:101-119) -> env_step()
+  * main_MFQ_Ising.py's episode loop (:84-159) and its numpy RandomState draws -> mfq()
+Pinned bit-exactly against tests/golden/ising_*.npz, which make_ising_fixtures.py recorded by
+running the reference's own Scenario / IsingWorld code.
+"""
+import numpy as np
+
+
+def neighbours(n_agents, view=1):
+    L = int(round(n_agents ** 0.5))
+    assert L * L == n_agents
+    idx = np.arange(n_agents)
+    r, c = idx // L, idx % L
+    cols = []
+    for d in range(1, view + 1):
+        for dr, dc in ((-d, 0), (d, 0), (0, -d), (0, d)):
+            cols.append(((r + dr) % L) * L + (c + dc) % L)
+    return np.sort(np.stack(cols, 1), axis=1)
+
+
+def env_step(spins, nbr, actions):
+    """spins/actions: [N] 0/1 -> (new spins, reward f64 [N], obs [N,K], n_up, order)."""
+    s = (np.asarray(actions) > 0).astype(np.int64)
+    pm = 2 * s - 1
+    nsum = pm[nbr].sum(axis=1).astype(np.float64)
+    reward = -((-0.5 * pm.astype(np.float64)) * nsum)
+    n_up = int(s.sum())
+    order = abs(n_up - (len(s) - n_up)) / (len(s) + 0.0)
+    return s, reward, s[nbr], n_up, order
+
+
+def mfq(n_agents, temperature, steps, lr=0.1, act_rate=1.0, decay_rate=0.99, decay_gap=2000, seed=13):
+    rs = np.random.RandomState(seed)
+    for _ in range(n_agents):                  # make_world -> reset_world
+        rs.choice(2)
+    spins = np.array([rs.choice(2) for _ in range(n_agents)], dtype=np.int64)   # env.reset()
+    nbr = neighbours(n_agents)
+    K = nbr.shape[1]
+    Q = np.zeros((n_agents, K + 1, 2))
+    current_t, max_order, done_ = 0.3, 0.0, 0
+    orders, nups, acts = [], [], []
+    n_upd = int(act_rate * n_agents)
+    ar = np.arange(n_agents)
+    for t in range(steps):
+        if t % decay_gap == 0:
+            current_t *= decay_rate
+        if current_t < temperature:
+            current_t = temperature
+        st = spins[nbr].sum(axis=1)
+        e0 = np.exp(Q[ar, st, 0] / current_t)
+        e1 = np.exp(Q[ar, st, 1] / current_t)
+        denom = e0 + e1
+        p0, p1 = e0 / denom, e1 / denom
+        c0 = p0 / (p0 + p1)
+        u = rs.random_sample(n_agents)
+        action = (u >= c0).astype(np.int64)
+        spins, reward, _obs, n_up, order = env_step(spins, nbr, action)
+        grp = rs.choice(n_agents, n_upd, replace=False)
+        Q[grp, st[grp], action[grp]] = Q[grp, st[grp], action[grp]] + lr * (reward[grp] - Q[grp, st[grp], action[grp]])
+        orders.append(order)
+        nups.append(n_up)
+        acts.append(action)
+        if order > max_order:
+            max_order = order
+        if abs(max_order - order) < 0.001:
+            done_ += 1
+        else:
+            done_ = 0
+        if done_ == 500:
+            break
+    return {"q": Q, "order": np.array(orders), "n_up": np.array(nups), "actions": np.stack(acts),
+            "spins": spins, "steps": len(orders)}

@@ -1,0 +1,115 @@
+"""Ising lattice + tabular MF-Q on the GPU (through the mfx_ising_* C ABI).
+
+* the fused MF-Q kernel in 'reference' mode reproduces the reference trajectories recorded in
+  tests/golden/ising_*.npz bit for bit: every action, order parameter, n_up, the early-stop
+  step and the float64 Q table;
+* the drop-in examples.ising_model env driven by main_MFQ_Ising.py's own loop gives the same;
+* the batched env step matches the numpy oracle on random lattices (R replicas);
+* Philox mode: ordered phase at low temperature, disordered at high temperature."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import common
+
+sys.path.insert(0, os.path.join(common.REPO, "oracle"))
+import ising_oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(common.GOLDEN, "ising_manifest.json")) as f:
+    CASES = json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_fused_mfq_matches_reference(name):
+    from mfrl_amd.ising import run_mfq
+    c = CASES[name]
+    fx = np.load(os.path.join(common.GOLDEN, name + ".npz"))
+    out = run_mfq(c["n_agents"], c["temperature"], c["steps"], lr=c["lr"], act_rate=c["act_rate"], seed=c["seed"])
+    T = c["stopped_after"]
+    assert int(out["steps"][0]) == T
+    assert out["order"][0, :T].tobytes() == fx["order"].tobytes()
+    np.testing.assert_array_equal(out["n_up"][0, :T], fx["n_up"])
+    np.testing.assert_array_equal(out["spins"][0], fx["spins"][-1])
+    assert out["q"][0].tobytes() == fx["q_final"].tobytes()
+
+
+def _main_loop_with_dropin(n_agents, temperature, steps, seed=13, lr=0.1):
+    """main_MFQ_Ising.py:11-159 (one episode), unchanged apart from the step count, on the drop-in."""
+    from examples.ising_model.multiagent.environment import IsingMultiAgentEnv
+    import examples.ising_model as ising_model
+    np.random.seed(seed)
+    scen = ising_model.load("Ising.py").Scenario()
+    env = IsingMultiAgentEnv(world=scen.make_world(num_agents=n_agents, agent_view=1),
+                             reset_callback=scen.reset_world, reward_callback=scen.reward,
+                             observation_callback=scen.observation, done_callback=scen.done)
+    n_actions = env.action_space[0].n
+    assert env.observation_space[0].n == 4
+    obs = np.stack(env.reset())
+    Q = np.zeros((env.n, 5, n_actions))
+    current_t = 0.3
+    acts = []
+    for t in range(steps):
+        action = np.zeros(env.n, dtype=np.int32)
+        if t % 2000 == 0:
+            current_t *= 0.99
+        if current_t < temperature:
+            current_t = temperature
+        for i in range(env.n):
+            s = np.count_nonzero(obs[i] == 1)
+            vals = [np.exp(Q[i, s, k] / current_t) for k in range(n_actions)]
+            denom = 0
+            for v in vals:
+                denom += v
+            action[i] = np.random.choice(n_actions, 1, p=[v / denom for v in vals])[0]
+        obs_, reward, done, order, ups, downs = env.step(np.expand_dims(action, axis=1))
+        obs_ = np.stack(obs_)
+        for i in np.random.choice(env.n, env.n, replace=False):
+            s = np.count_nonzero(obs[i] == 1)
+            Q[i, s, action[i]] = Q[i, s, action[i]] + lr * (reward[i][0] - Q[i, s, action[i]])
+        obs = obs_
+        acts.append(action.copy())
+    return np.stack(acts), Q
+
+
+def test_dropin_env_under_the_reference_loop():
+    c = CASES["ising10_t05"]
+    fx = np.load(os.path.join(common.GOLDEN, "ising10_t05.npz"))
+    T = 120
+    acts, Q = _main_loop_with_dropin(c["n_agents"], c["temperature"], T)
+    np.testing.assert_array_equal(acts, fx["actions"][:T])
+    q_at = list(fx["q_steps"]).index(T - 1 + 1) if (T) in list(fx["q_steps"] + 1) else None
+    if q_at is not None:
+        assert Q.tobytes() == fx["q"][q_at].tobytes()
+
+
+def test_env_step_matches_oracle_random():
+    from mfrl_amd.ising import IsingLattice
+    rs = np.random.RandomState(5)
+    for n, R in ((16, 3), (400, 8), (900, 2)):
+        lat = IsingLattice(n, replicas=R)
+        nbr = ising_oracle.neighbours(n)
+        lat.set_spins(rs.randint(0, 2, size=(R, n)))
+        acts = rs.randint(0, 2, size=(R, n))
+        rew, obs, nup, order = lat.step(acts)
+        for r in range(R):
+            s, rw, ob, nu, od = ising_oracle.env_step(None, nbr, acts[r])
+            assert rew[r].tobytes() == rw.tobytes()
+            np.testing.assert_array_equal(obs[r], ob)
+            assert nup[r] == nu and order[r] == od
+        np.testing.assert_array_equal(lat.get_spins(), acts)
+
+
+def test_philox_mode_phases():
+    from mfrl_amd.ising import run_mfq
+    cold = run_mfq(400, 0.3, 3000, mode="philox", replicas=8, seed=3)
+    hot = run_mfq(400, 5.0, 600, mode="philox", replicas=8, seed=3)
+    last = lambda o: np.array([o["order"][r, o["steps"][r] - 1] for r in range(8)])  # noqa: E731
+    # numpy oracle, same settings, 6 seeds: cold mean 0.43 (0.04..1.0), hot mean 0.045
+    assert last(cold).mean() > 0.25, last(cold)
+    assert last(hot).mean() < 0.15, last(hot)
+    assert last(cold).mean() > last(hot).mean() + 0.15
