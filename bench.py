@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=16384, help="envs per GPU")
     ap.add_argument("--max-steps", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
@@ -123,7 +123,8 @@ def main():
 
     eng = BattleBatch(MAP, args.envs, stream=stream)
     left, right = bd.block_positions(MAP, N_SIDE)
-    eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=1234 + rank)
+    from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing
+    eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     E = args.envs
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")
@@ -151,22 +152,15 @@ def main():
         ev[k][1].record(stream)
         if world > 1:          # episode statistics -> RCCL all-reduce (the only collective)
             eng.rollout_copy("stats", stats_buf)
-            red = stats_buf.view(E, 4).sum(0)
-            dist.all_reduce(red)
+            reduce_stats(stats_buf.view(E, 4))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     a1 = agent_steps()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    units = (a1 - a0).to(torch.float64).reshape(1)
     kernel_ms = sum(s.elapsed_time(e) for s, e in ev) / args.steps
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(units, op=dist.ReduceOp.SUM)
-    elapsed = float(elapsed.item())
-    total_units = float(units.item())
     local_units = float((a1 - a0).item())
+    elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         units_per_launch = local_units / args.steps

@@ -1,0 +1,136 @@
+/*
+ * magent_amd.h -- C ABI of the MI355X-native Battle / Ising mean-field engine (libmagent.so).
+ *
+ * Part 1 is the reference's own ABI, symbol for symbol: the 18 GridWorld entry points of
+ * examples/battle_model/src/runtime_api.h:118-181 (implemented at runtime_api.cc:15-169), so
+ * the reference python wrapper examples/battle_model/python/magent/gridworld.py (ctypes, no
+ * argtypes) and c_lib.py:13-31 bind this library unchanged.  Those calls act on env 0 and move
+ * data through caller-owned host buffers, exactly like the reference.
+ *
+ * Part 2 is this library's batched device API: E envs per engine, every buffer in HBM.
+ * Part 3 covers the Ising lattice / tabular MF-Q (the reference's examples/ising_model and
+ * main_MFQ_Ising.py are pure python; there is no reference ABI to mirror).
+ * Part 4 covers the mean-field training-loop kernels.
+ *
+ * Conventions: every function returns 0 on success and -1 on failure (message on stderr and in
+ * mfx_last_error()); the reference returns 0 and aborts on fatal errors instead.  "d_" pointers
+ * are device pointers, the others host pointers.  Streams are hipStream_t passed as void*.
+ */
+#ifndef MAGENT_AMD_H
+#define MAGENT_AMD_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- part 1: reference ABI */
+/* runtime_api.h:118 env_new_game -- name must be "GridWorld" (DiscreteSnake is out of scope) */
+int env_new_game(void **game, const char *name);
+/* runtime_api.h:119 */
+int env_delete_game(void *game);
+/* runtime_api.h:120 -- keys of GridWorld::set_config (GridWorld.cc:126-155): map_width,
+ * map_height (int*), minimap_mode (bool*), embedding_size (int*), render_dir (char*),
+ * seed (int*); food_mode / turn_mode / goal_mode must stay false */
+int env_config_game(void *game, const char *key, void *value);
+/* runtime_api.h:123 */
+int env_reset(void *game);
+/* runtime_api.h:124 -- bufs[0] = float[n][view_h][view_w][n_ch], bufs[1] = float[n][feature] */
+int env_get_observation(void *game, int group, float **bufs);
+/* runtime_api.h:125 -- actions int32[n] in group-vector order */
+int env_set_action(void *game, int group, const int *actions);
+/* runtime_api.h:126 */
+int env_step(void *game, int *done);
+/* runtime_api.h:127 -- float[n] */
+int env_get_reward(void *game, int group, float *buffer);
+/* runtime_api.h:130 -- num, id, pos, alive, action_space, view_space, feature_space,
+ * view2attack, attack_base, both_attack (GridWorld.cc:777-978) */
+int env_get_info(void *game, int group, const char *name, void *buffer);
+/* runtime_api.h:133-134 -- rendering is out of scope: accepted, no-op */
+int env_render(void *game);
+int env_render_next_file(void *game);
+/* runtime_api.h:140 -- AgentType reflection keys (AgentType.cc:63-101) */
+int gridworld_register_agent_type(void *game, const char *name, int n, const char **keys, float *values);
+/* runtime_api.h:141 */
+int gridworld_new_group(void *game, const char *agent_type_name, int *group);
+/* runtime_api.h:142-143 -- method "custom" | "random" | "fill"; group -1 = walls */
+int gridworld_add_agents(void *game, int group, int n, const char *method, const int *pos_x, const int *pos_y,
+                         const int *dir);
+/* runtime_api.h:146 */
+int gridworld_clear_dead(void *game);
+/* runtime_api.h:147 -- deprecated in the reference; returns -1 */
+int gridworld_set_goal(void *game, int group, const char *method, const int *linear_buffer);
+/* runtime_api.h:150-153 -- reward DSL.  Supported: rules triggered by one attack / kill /
+ * collide event between 'any' agents of two groups, rewarding its subject and/or object.
+ * The reference python passes 6 arguments to the 7-parameter add_reward_rule; auto_value is
+ * never read (RewardEngine.cc:252 reads it for OP_ALIGN only). */
+int gridworld_define_agent_symbol(void *game, int no, int group, int index);
+int gridworld_define_event_node(void *game, int no, int op, int *inputs, int n_inputs);
+int gridworld_add_reward_rule(void *game, int on, int *receiver, float *value, int n_receiver, bool is_terminal,
+                              bool auto_value);
+
+/* ---------------------------------------------------------------- part 2: batched Battle */
+/* Before the first env_reset: make the engine hold n_envs identical envs. */
+int mfx_battle_set_num_envs(void *game, int n_envs);
+/* Launch everything on this hipStream_t (may be the null stream). */
+int mfx_battle_set_stream(void *game, void *stream);
+/* Per-call API on device buffers; per-agent arrays are [E][rowcap][...]. */
+int mfx_battle_observe(void *game, int group, float *d_view, float *d_feature, int rowcap);
+int mfx_battle_set_action(void *game, int group, const int *d_actions, int rowcap);
+int mfx_battle_step(void *game, int *d_done);
+/* what: 0 num ([E]), 1 reward (f32), 2 id (i32), 3 alive (u8), 4 pos (i32 x2), 5 hp (f32) */
+int mfx_battle_get(void *game, int group, int what, void *d_out, int rowcap);
+int mfx_battle_clear_dead(void *game);
+/* Wait for the stream and report any device-side error (capacity, bad action, ...). */
+int mfx_battle_sync(void *game);
+/* Upper bound of a group's size (rows needed per env). */
+int mfx_battle_group_capacity(void *game, int group, int *cap);
+/* Fused rollout: one launch per training-loop step for all envs (obs for every group, on-device
+ * rush policy, set_action, step, reward, mean action, clear_dead, restart at done / max_steps).
+ * tmpl_n[G], xs[G][tmpl_n[g]], ys[...]: placement re-applied at every episode start. */
+int mfx_battle_rollout_init(void *game, const int *tmpl_n, const int *const *xs, const int *const *ys,
+                            int max_steps, float eps, unsigned seed, int stagger);
+int mfx_battle_rollout_step(void *game, int n_steps);
+/* names: view, feature, actions, rewards, mean_action, episode_return, stats, agent_steps, group_num */
+int mfx_battle_rollout_buffer(void *game, const char *name, int group, void **d_ptr, size_t *bytes);
+int mfx_battle_rollout_copy(void *game, const char *name, int group, void *dst, size_t bytes);
+int mfx_battle_rollout_rowcap(void *game, int *rowcap);
+/* Diagnostic build only (libmagent_stamps.so): per-phase s_memtime stamps [E][16]. */
+int mfx_battle_set_stamp_buffer(void *d_buf);
+
+/* ---------------------------------------------------------------- part 3: Ising MF-Q */
+int mfx_ising_create(int replicas, int n_agents, int k, const int16_t *nbr, void **handle);
+int mfx_ising_destroy(void *handle);
+int mfx_ising_set_spins(void *handle, const uint8_t *spins);
+int mfx_ising_get_spins(void *handle, uint8_t *spins);
+/* IsingMultiAgentEnv.step for every replica (environment.py:49-78) */
+int mfx_ising_step(void *handle, const int32_t *actions, double *reward, uint8_t *obs, int32_t *n_up,
+                   double *order);
+/* The episode loop of main_MFQ_Ising.py (:84-159) in one launch per batch of replicas. */
+int mfx_ising_mfq_run(void *handle, int T, double temperature, double lr, double decay_rate, int decay_gap,
+                      const double *u, const uint32_t *mask, unsigned seed, double *q, double *order,
+                      int32_t *n_up, int32_t *steps);
+
+/* ---------------------------------------------------------------- part 4: mean-field kernels */
+/* senario_battle.py:141 */
+int mfx_mean_action(const int32_t *d_acts, const int32_t *d_counts, int B, int rowcap, int n_action, double *d_out,
+                    void *stream);
+/* algo/base.py:192-220 */
+int mfx_mfq_target(const float *d_eq, const float *d_tq, const float *d_r, const uint8_t *d_done, int M, int A,
+                   double gamma, double *d_out, void *stream);
+/* algo/ac.py:305-320 */
+int mfx_mfac_returns(float *d_rew, const int64_t *d_offsets, const float *d_value, int n_ep, float gamma,
+                     void *stream);
+
+/* ---------------------------------------------------------------- library */
+const char *mfx_last_error(void);
+const char *mfx_build_info(void);
+int mfx_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAGENT_AMD_H */

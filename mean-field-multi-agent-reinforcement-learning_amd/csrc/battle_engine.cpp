@@ -19,6 +19,7 @@
 #include "battle_kernels.h"
 #include "battle_layout.h"
 #include "mfx_common.h"
+#include "../../include/magent_amd.h"
 
 namespace mfx {
 

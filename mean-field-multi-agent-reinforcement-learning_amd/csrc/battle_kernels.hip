@@ -942,7 +942,8 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParam
         __syncthreads();
         for (int t = threadIdx.x; t < G * 64; t += blockDim.x) {
             const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
-            if (k < na) ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : 0.0;
+            if (k < na)   // empty group: np.mean of nothing is NaN
+                ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
         }
     }
     MFX_STAMP(4);

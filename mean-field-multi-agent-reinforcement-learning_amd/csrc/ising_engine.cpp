@@ -10,6 +10,7 @@
 
 #include "ising_kernels.h"
 #include "mfx_common.h"
+#include "../../include/magent_amd.h"
 
 namespace mfx {
 

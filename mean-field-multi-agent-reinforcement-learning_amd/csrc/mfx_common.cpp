@@ -1,5 +1,6 @@
 // mfx_common.cpp -- last-error storage and library-level queries of the C ABI.
 #include "mfx_common.h"
+#include "../../include/magent_amd.h"
 
 #include <hip/hip_runtime.h>
 

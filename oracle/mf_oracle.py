@@ -1,0 +1,30 @@
+"""TEST ORACLE ONLY -- the mean-field training-loop expressions, restated from the reference's source
+text in numpy (tests may use it; the product never does).
+
+* mean_action  -- senario_battle.py:141, the reference expression verbatim in meaning.  Pinned:
+                  tests/golden/battle_*.npz hold its value on every recorded step.
+* mfq_target   -- algo/base.py:208-220 (ValueNet.calc_target_q after the TF session call).
+* mfac_returns -- algo/ac.py:305-320 (MFAC.train's backward return loop).
+  The last two are PARITY UNPINNED: algo/ imports tensorflow, which this image lacks, so no
+  reference output exists for them; they are checked against this source-text restatement only.
+"""
+import numpy as np
+
+
+def mean_action(acts, n_action):
+    return np.mean(list(map(lambda x: np.eye(n_action)[x], acts)), axis=0, keepdims=True)
+
+
+def mfq_target(e_q, t_q, rewards, dones, gamma=0.95):
+    act_idx = np.argmax(e_q, axis=1)
+    q_values = t_q[np.arange(len(t_q)), act_idx]
+    return rewards + (1. - dones) * q_values.reshape(-1) * gamma
+
+
+def mfac_returns(rewards, value, gamma=0.95):
+    r = np.array(rewards, dtype=np.float32)
+    keep = np.float32(value)
+    for i in reversed(range(len(r))):
+        keep = keep * gamma + r[i]
+        r[i] = keep
+    return r
