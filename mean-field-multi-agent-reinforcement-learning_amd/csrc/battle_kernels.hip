@@ -189,6 +189,7 @@ struct ObsSmem {                  // LDS carve-up of the observation kernels
     uint16_t* bin;                // [cap] minimap cell of every agent id (this call)
     uint8_t* mask;                // [VH*VW]
     float* type_hp;               // [G]
+    float* hpn;                   // [cap] hp / max hp of every id (wave-streamed path), or null
 };
 
 // Battle fast path (builtin/config/battle.py): 13x13 view, 7 channels, 2 groups, minimap, 34
@@ -212,6 +213,8 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
             const int b = ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw;
             sm.bin[id] = (uint16_t)b;
             atomicAdd(&sm.hist[j * NV + b], 1);
+            // hp / max hp (Map.cc:208), once per agent instead of once per viewer
+            if (sm.hpn) sm.hpn[id] = v.hp[id] / gp.type[j].hp;
         }
     }
     __syncthreads();
@@ -310,33 +313,128 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     __syncthreads();
 }
 
+// ---- Battle fast path, wave-streamed: every wave takes 64 consecutive view cells of the group's
+// output stream (row a, cell c -> stream cell a*169+c), one per lane, computes the cell's 7
+// channels, transposes them through its own 1792-B LDS slice and stores them as 112 float4s
+// (1 KiB contiguous per store instruction).  No workgroup barrier anywhere in the phase.
+constexpr int kWaveCells = 64;
+constexpr int kWaveStageFloats = kWaveCells * BattleShape::NC;   // 448 floats = 1792 B per wave
+
+__device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int g,
+                                                  int n, float* __restrict__ out_view, float* __restrict__ out_feat,
+                                                  float* wave_stage) {
+    constexpr int NV = BattleShape::VW * BattleShape::VH, NC = BattleShape::NC, F = BattleShape::F;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int W = gp.W, H = gp.H;
+    const TypeParams& T = gp.type[g];
+    const int vx1 = T.view_x1, vy1 = T.view_y1;
+    const int32_t* ids = v.grp_ids + g * v.cap;
+    const float* mm_own = sm.mm + g * NV;
+    const float* mm_en = sm.mm + (g ^ 1) * NV;
+    float* st = wave_stage + wid * kWaveStageFloats;
+    const int ncell = n * NV;
+    for (int base = wid * kWaveCells; base < ncell; base += nw * kWaveCells) {
+        const int gc = base + lane;
+        float x[NC];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) x[k] = 0.0f;
+        if (gc < ncell) {
+            const int a = gc / NV, c = gc - a * NV;
+            const int vy = c / BattleShape::VW, vx = c - vy * BattleShape::VW;
+            const int id = ids[a];
+            const uint32_t pos = v.xy[id];
+            const int mx = (int)(pos & 0xFFFF) + vx1 + vx, my = (int)(pos >> 16) + vy1 + vy;
+            if (sm.mask[c] && mx >= 0 && my >= 0 && mx < W && my < H) {
+                const uint32_t cv = v.cells[my * W + mx];
+                if (cv == kCellWall) {
+                    x[0] = 1.0f;
+                } else if (cv != kCellEmpty) {
+                    const float hn = sm.hpn[cv];
+                    if ((int)meta_group(v.meta[cv]) == g) { x[1] = 1.0f; x[2] = hn; }
+                    else { x[4] = 1.0f; x[5] = hn; }
+                }
+            }
+            const bool self = c == (int)sm.bin[id];
+            const float mo = mm_own[c], me = mm_en[c];
+            x[3] = self ? mo + 1.0f : mo;
+            x[6] = self ? me + 1.0f : me;
+        }
+#pragma unroll
+        for (int k = 0; k < NC; ++k) st[lane * NC + k] = x[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int cells = min(kWaveCells, ncell - base);
+        float* dst = out_view + (size_t)base * NC;        // base % 64 == 0 -> 16-B aligned
+        if (cells == kWaveCells) {
+            const float4* s4 = reinterpret_cast<const float4*>(st);
+            float4* d4 = reinterpret_cast<float4*>(dst);
+            d4[lane] = s4[lane];
+            if (lane < kWaveStageFloats / 4 - 64) d4[64 + lane] = s4[64 + lane];
+        } else {
+            for (int i = lane; i < cells * NC; i += 64) dst[i] = st[i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // features (GridWorld.cc:411-421): consecutive lanes write consecutive floats
+    const int emb = gp.emb, na = T.n_action;
+    for (int p = threadIdx.x; p < n * F; p += blockDim.x) {
+        const int a = p / F, f = p - a * F;
+        const int id = ids[a];
+        float val = 0.0f;
+        if (f < emb) val = (float)((id >> f) & 1);
+        if (f == emb + v.last_act[id]) val = 1.0f;
+        if (f == emb + na) val = v.last_r[id];
+        const uint32_t pos = v.xy[id];
+        if (f == emb + na + 1) val = (float)(int)(pos & 0xFFFF) / (float)W;
+        if (f == emb + na + 2) val = (float)(int)(pos >> 16) / (float)H;
+        out_feat[p] = val;
+    }
+}
+
 __host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
     if (gp.n_groups != BattleShape::G || !gp.minimap || gp.n_ch != BattleShape::NC) return false;
-    for (int g = 0; g < gp.n_groups; ++g)
+    for (int g = 0; g < gp.n_groups; ++g) {
         if (gp.type[g].view_w != BattleShape::VW || gp.type[g].view_h != BattleShape::VH ||
-            gp.feat_size[g] != BattleShape::F)
+            gp.feat_size[g] != BattleShape::F || gp.type[g].view_x1 != gp.type[0].view_x1 ||
+            gp.type[g].view_y1 != gp.type[0].view_y1)
             return false;
+        for (int c = 0; c < BattleShape::VW * BattleShape::VH; ++c)
+            if (gp.type[g].view_mask[c] != gp.type[0].view_mask[c]) return false;
+    }
     return true;
 }
 
-__host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int cap) {
+// LDS of the observation phase.  stage_floats: the staging area (K rows for the staged path,
+// one 448-float slice per wave for the wave-streamed path).
+__host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int cap, size_t stage_floats) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t NV = (size_t)gp.type[g].view_w * gp.type[g].view_h;
-    return (size_t)kObsK * NV * gp.n_ch * 4 + (((size_t)gp.n_groups * NV * 4 + 15) & ~(size_t)15) +
-           (((size_t)cap * 2 + 15) & ~(size_t)15) + 16 + ((NV + 15) & ~(size_t)15);
+    return r16(stage_floats * 4) + r16((size_t)gp.n_groups * NV * 4) + r16((size_t)cap * 2) + 16 + r16(NV) +
+           r16((size_t)cap * 4);
 }
 
-__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, int cap, size_t& off) {
+__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, int cap, size_t stage_floats,
+                                             size_t& off) {
     const TypeParams& T = gp.type[g];
     const size_t NV = (size_t)T.view_w * T.view_h, G = gp.n_groups;
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     ObsSmem sm;
-    sm.stage = reinterpret_cast<float*>(smem + off); off += (size_t)kObsK * NV * gp.n_ch * 4;
+    sm.stage = reinterpret_cast<float*>(smem + off); off += r16(stage_floats * 4);
     sm.mm = reinterpret_cast<float*>(smem + off);    // the histogram is converted in place
     sm.hist = reinterpret_cast<int*>(smem + off);    off += r16(G * NV * 4);
     sm.bin = reinterpret_cast<uint16_t*>(smem + off); off += r16((size_t)cap * 2);
     sm.type_hp = reinterpret_cast<float*>(smem + off); off += 16;
     sm.mask = reinterpret_cast<uint8_t*>(smem + off); off += r16(NV);
+    sm.hpn = reinterpret_cast<float*>(smem + off);   off += r16((size_t)cap * 4);
     return sm;
+}
+
+__host__ __device__ inline size_t obs_stage_floats(const GameParams& gp, int g, bool wave_streamed, int threads) {
+    return wave_streamed ? (size_t)(threads / 64) * kWaveStageFloats
+                         : (size_t)kObsK * gp.type[g].view_w * gp.type[g].view_h * gp.n_ch;
 }
 
 __device__ __forceinline__ void obs_prologue(const GameParams& gp, const ObsSmem& sm, int g) {
@@ -362,7 +460,8 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     const int a_end = min(n, a_begin + chunk);
     if (a_end > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
     size_t off = 0;
-    ObsSmem sm = carve_obs(smem, gp, g, s.cap, off);
+    ObsSmem sm = carve_obs(smem, gp, g, s.cap, obs_stage_floats(gp, g, kB, blockDim.x), off);
+    if (!kB) sm.hpn = nullptr;
     if (cells_in_lds) {
         uint16_t* lc = reinterpret_cast<uint16_t*>(smem + off);
         const int n2 = s.cells_n;
@@ -373,9 +472,16 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     obs_minimap<kB>(gp, v, sm);
     const TypeParams& T = gp.type[g];
     const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
+    const int F = gp.feat_size[g];
     float* ov = out_view + (size_t)e * rowcap * VF;
-    float* of = out_feat + (size_t)e * rowcap * gp.feat_size[g];
-    for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows<kB>(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
+    float* of = out_feat + (size_t)e * rowcap * F;
+    if (kB) {
+        EnvView vc = v;                      // rows [a_begin, a_end): shift the group list and outputs
+        vc.grp_ids = v.grp_ids + a_begin;
+        obs_stream_battle(gp, vc, sm, g, a_end - a_begin, ov + (size_t)a_begin * VF, of + (size_t)a_begin * F, sm.stage);
+    } else {
+        for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows<kB>(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
+    }
 }
 
 // ==================================================================================
@@ -800,37 +906,39 @@ __device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-o
     return r;
 }
 
-// LDS plan of k_rollout: the env (cells, per-id arrays, group lists) + the observation scratch.
-// The staging buffer of the observation rounds is dead once the last row is streamed out, so the
-// policy actions, action histogram, attack/move buffers and the reduction area reuse it.
+// LDS plan of k_rollout: the env (cells, per-id arrays, group lists) stays resident for the whole
+// launch; one scratch region is shared by the observation phase (minimap, bins, hp/max, staging) and
+// the policy/step phase (actions, histogram, attack/move buffers; the reduction reuses the actions).
 struct RolloutUnion { size_t act, ahist, atk, mov, sorted, red, total; };
 
-__host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int cap, int acap) {
+__host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int cap, int acap, int threads) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     RolloutUnion u;
     size_t o = 0;
-    u.act = o;    o += r16((size_t)gp.n_groups * cap * 4);
+    u.act = o;    o += r16((size_t)(gp.n_groups * cap > threads ? gp.n_groups * cap : threads) * 4);
+    u.red = u.act;                                 // block_sum after the step: the actions are dead
     u.ahist = o;  o += r16((size_t)gp.n_groups * 64 * 4);
     u.atk = o;    o += r16((size_t)acap * 4);
     u.mov = o;    o += r16((size_t)acap * 4);
     u.sorted = o; o += gp.large_map ? r16((size_t)acap * 4) : 0;
-    u.red = o;    o += r16(1024 * 4);                  // block_sum scratch, up to 1024 threads
     u.total = o;
     return u;
+}
+
+__host__ __device__ inline size_t rollout_scratch_bytes(const GameParams& gp, int cap, int acap, int threads) {
+    const size_t obs = obs_smem_core(gp, 0, cap, obs_stage_floats(gp, 0, is_battle_shape(gp), threads));
+    const size_t stp = rollout_union(gp, cap, acap, threads).total;
+    return obs > stp ? obs : stp;
 }
 
 size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const int G = gp.n_groups;
-    const size_t NV = (size_t)gp.type[0].view_w * gp.type[0].view_h;
-    const size_t stage = (size_t)kObsK * NV * gp.n_ch * 4;
     size_t b = r16((size_t)cells_n * 2);
     b += 6 * r16((size_t)cap * 4) + r16(cap);             // xy hp next_r last_r last_act op_obj + meta
     b += r16((size_t)G * cap * 4);                         // grp_ids
     b += 4 * r16(G * 4);                                   // grp_n grp_dead grp_reward n_before
-    b += obs_smem_core(gp, 0, cap);                        // includes the staging buffer
-    const RolloutUnion u = rollout_union(gp, cap, acap);
-    if (u.total > stage) b += r16(u.total - stage);
+    b += rollout_scratch_bytes(gp, cap, acap, 256);
     return b;
 }
 
@@ -870,9 +978,11 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParam
     v.grp_dead = reinterpret_cast<int32_t*>(carve(G * 4));
     v.grp_reward = reinterpret_cast<float*>(carve(G * 4));
     int32_t* n_before = reinterpret_cast<int32_t*>(carve(G * 4));
-    ObsSmem osm = carve_obs(smem, gp, 0, cap, off);
-    const RolloutUnion u = rollout_union(gp, cap, acap);
-    char* uni = reinterpret_cast<char*>(osm.stage);
+    char* uni = smem + off;                 // scratch shared by the observation and the step phases
+    size_t soff = off;
+    ObsSmem osm = carve_obs(smem, gp, 0, cap, obs_stage_floats(gp, 0, kB, blockDim.x), soff);
+    if (!kB) osm.hpn = nullptr;
+    const RolloutUnion u = rollout_union(gp, cap, acap, blockDim.x);
     int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
     int* ahist = reinterpret_cast<int*>(uni + u.ahist);
     uint32_t* atk = reinterpret_cast<uint32_t*>(uni + u.atk);
@@ -909,18 +1019,24 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParam
     __syncthreads();
     MFX_STAMP(1);
     // ---------------- get_observation for every group
+    obs_prologue(gp, osm, 0);
     obs_minimap<kB>(gp, v, osm);
     MFX_STAMP(2);
     for (int g = 0; g < G; ++g) {
-        obs_prologue(gp, osm, g);
-        __syncthreads();
         const TypeParams& T = gp.type[g];
         const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
         float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
         float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
         const int n = min(v.grp_n[g], ra.rowcap);
-        for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
+        if (kB) {
+            obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
+        } else {
+            obs_prologue(gp, osm, g);
+            __syncthreads();
+            for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
+        }
     }
+    __syncthreads();                       // the scratch region changes hands
     MFX_STAMP(3);
     // ---------------- policy + mean action (former_act_prob), all groups in one pass
     {
@@ -1058,7 +1174,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParam
 //  host-side launchers
 // ==================================================================================
 size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n, int cap) {
-    size_t b = obs_smem_core(gp, g, cap);
+    size_t b = obs_smem_core(gp, g, cap, obs_stage_floats(gp, g, is_battle_shape(gp), 256));
     if (cells_in_lds) b += (size_t)cells_n * 2;
     return b;
 }
