@@ -98,6 +98,8 @@ int mfx_battle_rollout_step(void *game, int n_steps);
 int mfx_battle_rollout_buffer(void *game, const char *name, int group, void **d_ptr, size_t *bytes);
 int mfx_battle_rollout_copy(void *game, const char *name, int group, void *dst, size_t bytes);
 int mfx_battle_rollout_rowcap(void *game, int *rowcap);
+/* Persistent grid (workgroups per launch) and dynamic LDS bytes per workgroup of the fused rollout. */
+int mfx_battle_rollout_info(void *game, int *grid, int *lds_bytes);
 /* Diagnostic build only (libmagent_stamps.so): per-phase s_memtime stamps [E][16]. */
 int mfx_battle_set_stamp_buffer(void *d_buf);
 

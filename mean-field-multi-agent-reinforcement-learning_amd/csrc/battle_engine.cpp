@@ -132,6 +132,12 @@ public:
     DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
     DevBuf<double> ro_mean, ro_stats;
     DevBuf<unsigned long long> ro_steps;
+    DevBuf<int32_t> ro_work;                 // k_rollout work-queue counters (2)
+    DevBuf<int32_t> ro_order;                // k_rollout queue order (k_env_order)
+    DevBuf<uint4> ro_image;                  // reset image (k_reset_image)
+    DevBuf<RolloutCtx> ro_ctx;               // device copy of {s, ra} read by k_rollout
+    RolloutCtx ro_ctx_host{};
+    int ro_grid = 0, ro_cap = 0;
 
     ~BattleEngine() { release(); if (own_stream && stream) (void)hipStreamDestroy(stream); }
 
@@ -509,16 +515,48 @@ public:
         }
         MFX_CHECK(reset());
         for (int g = 0; g < G; g++) MFX_CHECK(add_agents(g, tmpl_n[g], "custom", xs[g], ys[g]));
+        MFX_CHECK(rollout_plan());
         rollout_ready = true;
+        return 0;
+    }
+
+    // Reset image, work queue and persistent grid for the current capacity.
+    int rollout_plan() {
+        try {
+            ro_work.ensure(2);
+            MFX_HIP_THROW(hipMemsetAsync(ro_work.p, 0, 2 * sizeof(int32_t), stream));
+            ro_image.ensure((rollout_reset_image_bytes(gp, s.cells_n, s.cap) + 15) / 16);
+            ro_order.ensure(E);
+            ra.work = ro_work.p; ra.work_sel = 0; ra.reset_image = ro_image.p; ra.order = ro_order.p;
+            MFX_HIP_THROW(launch_reset_image(gp, d_gp, s, ra, ro_image.p, stream));
+            MFX_HIP_THROW(rollout_grid(gp, s, &ro_grid));
+            ro_cap = s.cap;
+            ro_ctx.ensure(1);
+            ro_ctx_host.s = s; ro_ctx_host.ra = ra;
+            MFX_HIP_THROW(hipMemcpyAsync(ro_ctx.p, &ro_ctx_host, sizeof(RolloutCtx), hipMemcpyHostToDevice, stream));
+            MFX_HIP_THROW(hipStreamSynchronize(stream));
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
         return 0;
     }
 
     int rollout_step(int n_steps) {
         if (!rollout_ready) return fail("rollout_step before rollout_init");
+        if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
         for (int i = 0; i < n_steps; i++) {
-            MFX_HIP(launch_rollout(gp, d_gp, s, ra, stream));
+            MFX_HIP(launch_env_order(s, n_groups(), ro_order.p, stream));
+            MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.step_index, ra.work_sel, ro_grid, stream));
             ra.step_index++;
+            ra.work_sel ^= 1;
         }
+        return 0;
+    }
+
+    int rollout_info(int* grid, int* lds_bytes) {
+        if (!rollout_ready) return fail("rollout_info before rollout_init");
+        *grid = ro_grid;
+        *lds_bytes = (int)rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
         return 0;
     }
 
@@ -752,6 +790,11 @@ MFX_API int mfx_battle_set_stamp_buffer(void* d_buf) {
     MFX_HIP(mfx::set_stamp_buffer((unsigned long long*)d_buf));
     return 0;
 }
+// Launch geometry of the fused rollout: persistent grid (workgroups) and LDS bytes per workgroup.
+MFX_API int mfx_battle_rollout_info(void* game, int* grid, int* lds_bytes) {
+    MFX_GUARD(MFX_ENV(game)->rollout_info(grid, lds_bytes));
+}
+
 MFX_API int mfx_battle_rollout_rowcap(void* game, int* rowcap) {
     *rowcap = MFX_ENV(game)->ra.rowcap;
     return 0;

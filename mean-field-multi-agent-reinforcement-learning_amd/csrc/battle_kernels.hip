@@ -25,13 +25,36 @@ __device__ unsigned long long* g_stamps;
 #define MFX_STAMP(i)                                                                        \
     do {                                                                                    \
         __syncthreads();                                                                    \
-        if (threadIdx.x == 0 && g_stamps) g_stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (TID == 0 && g_stamps) {                                                         \
+            g_stamps[stamp_row * 16 + (i)] = __builtin_amdgcn_s_memtime();                  \
+            if ((i) == 0) g_stamps[stamp_row * 16 + 11] = __builtin_amdgcn_s_memrealtime();  \
+            if ((i) == 10) g_stamps[stamp_row * 16 + 12] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                   \
     } while (0)
 #else
 #define MFX_STAMP(i) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- utils
+// Lane id in the workgroup, opaque to loop-invariant code motion: k_rollout is one long loop over
+// envs, and every address derived from the lane id would otherwise be hoisted out of it and kept
+// live (in VGPRs) for the whole launch.
+__device__ __forceinline__ int mfx_tid() {
+    int t = (int)__builtin_amdgcn_workitem_id_x();
+    asm volatile("" : "+v"(t));
+    return t;
+}
+#define TID mfx_tid()
+
+// Read-only HBM struct seen through the constant address space with an opaque pointer: field reads
+// become scalar loads at their use instead of values hoisted out of a loop and pinned in SGPRs.
+template <class T>
+__device__ __forceinline__ const T& kconst(const T* p) {
+    auto q = (const __attribute__((address_space(4))) T*)p;
+    asm volatile("" : "+s"(q));
+    return *(const T*)q;
+}
+
 __device__ __forceinline__ uint32_t minstd_next(uint32_t x) {   // minstd_rand0, GridWorld.h:106
     uint64_t p = (uint64_t)x * 16807u;
     p = (p & 0x7FFFFFFFull) + (p >> 31);
@@ -43,7 +66,7 @@ __device__ __forceinline__ void set_err(const State& s, int code) { atomicCAS(s.
 
 // Exclusive scan of a 0/1 flag over the workgroup (blockDim multiple of 64, <= 1024).
 __device__ __forceinline__ int block_scan_flag(int flag, int* wave_tot, int& total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = TID & 63, wid = TID >> 6, nw = blockDim.x >> 6;
     const unsigned long long m = __ballot(flag);
     const int pre = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) wave_tot[wid] = __popcll(m);
@@ -96,16 +119,16 @@ __device__ __forceinline__ EnvView global_view(const State& s, int e, int G) {
 __global__ void __launch_bounds__(256) k_reset(const GameParams* __restrict__ gp, State s) {
     const int e = blockIdx.x, W = gp->W, H = gp->H, G = gp->n_groups;
     uint16_t* cells = s.cells + (size_t)e * s.cells_n;
-    for (int c = threadIdx.x; c < W * H; c += blockDim.x) {
+    for (int c = TID; c < W * H; c += blockDim.x) {
         const int x = c % W, y = c / W;
         cells[c] = (x == 0 || y == 0 || x == W - 1 || y == H - 1) ? kCellWall : kCellEmpty;
     }
-    if (threadIdx.x < G) {
-        s.grp_n[e * G + threadIdx.x] = 0;
-        s.grp_dead[e * G + threadIdx.x] = 0;
-        s.grp_reward[e * G + threadIdx.x] = 0.0f;
+    if (TID < G) {
+        s.grp_n[e * G + TID] = 0;
+        s.grp_dead[e * G + TID] = 0;
+        s.grp_reward[e * G + TID] = 0.0f;
     }
-    if (threadIdx.x == 0) { s.id_counter[e] = 0; s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = 0; }
+    if (TID == 0) { s.id_counter[e] = 0; s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = 0; }
 }
 
 __device__ __forceinline__ bool is_blank(const uint16_t* cells, int W, int H, int x, int y, int self) {
@@ -119,7 +142,7 @@ __device__ __forceinline__ bool is_blank(const uint16_t* cells, int W, int H, in
 // id is not consumed -- GridWorld.cc:180-187).  method: 0 custom, 1 random, 2 fill.
 __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int group, int n, int method,
                              const int* __restrict__ xs, const int* __restrict__ ys, int per_env_stride) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = blockIdx.x * blockDim.x + TID;
     if (e >= s.E) return;
     const int W = gp->W, H = gp->H, G = gp->n_groups;
     EnvView v = global_view(s, e, G);
@@ -203,11 +226,11 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
     const int VW = kB ? BattleShape::VW : T0.view_w, VH = kB ? BattleShape::VH : T0.view_h;
     const int G = kB ? BattleShape::G : gp.n_groups, NV = VW * VH;
     const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
-    for (int i = threadIdx.x; i < G * NV; i += blockDim.x) sm.hist[i] = 0;
+    for (int i = TID; i < G * NV; i += blockDim.x) sm.hist[i] = 0;
     __syncthreads();
     for (int j = 0; j < G; ++j) {
         const int n = v.grp_n[j];
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        for (int i = TID; i < n; i += blockDim.x) {
             const int id = v.grp_ids[j * v.cap + i];
             const uint32_t p = v.xy[id];
             const int b = ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw;
@@ -218,7 +241,7 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < G * NV; i += blockDim.x) {   // in place: mm aliases hist
+    for (int i = TID; i < G * NV; i += blockDim.x) {   // in place: mm aliases hist
         const int j = i / NV;
         const int n = v.grp_n[j];
         // 0/0 gives the x86 default NaN (0xFFC00000) in the reference; reproduce its bits.
@@ -241,7 +264,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     const int per = MM ? 3 : 2;
     const int32_t* ids = v.grp_ids + g * v.cap;
     // ---- phase 1: one lane per (agent, view cell) computes that cell's NC channels
-    for (int p = threadIdx.x; p < k * NV; p += blockDim.x) {
+    for (int p = TID; p < k * NV; p += blockDim.x) {
         const int al = p / NV, c = p - al * NV;
         const int vy = c / VW, vx = c - vy * VW;
         const int id = ids[a0 + al];
@@ -283,7 +306,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     // ---- features (GridWorld.cc:411-421): written straight out, consecutive lanes = consecutive floats
     const int F = kB ? BattleShape::F : gp.feat_size[g];
     const int emb = gp.emb, na = T.n_action;
-    for (int p = threadIdx.x; p < k * F; p += blockDim.x) {
+    for (int p = TID; p < k * F; p += blockDim.x) {
         const int al = p / F, f = p - al * F;
         const int id = ids[a0 + al];
         float val = 0.0f;
@@ -305,10 +328,10 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
         const int n4 = nf >> 2;
         const float4* src4 = reinterpret_cast<const float4*>(sm.stage);
         float4* dst4 = reinterpret_cast<float4*>(dst);
-        for (int i = threadIdx.x; i < n4; i += blockDim.x) dst4[i] = src4[i];
-        for (int i = (n4 << 2) + threadIdx.x; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
+        for (int i = TID; i < n4; i += blockDim.x) dst4[i] = src4[i];
+        for (int i = (n4 << 2) + TID; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
     } else {
-        for (int i = threadIdx.x; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
+        for (int i = TID; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
     }
     __syncthreads();
 }
@@ -324,7 +347,7 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
                                                   int n, float* __restrict__ out_view, float* __restrict__ out_feat,
                                                   float* wave_stage) {
     constexpr int NV = BattleShape::VW * BattleShape::VH, NC = BattleShape::NC, F = BattleShape::F;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = TID & 63, wid = TID >> 6, nw = blockDim.x >> 6;
     const int W = gp.W, H = gp.H;
     const TypeParams& T = gp.type[g];
     const int vx1 = T.view_x1, vy1 = T.view_y1;
@@ -380,7 +403,7 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
     }
     // features (GridWorld.cc:411-421): consecutive lanes write consecutive floats
     const int emb = gp.emb, na = T.n_action;
-    for (int p = threadIdx.x; p < n * F; p += blockDim.x) {
+    for (int p = TID; p < n * F; p += blockDim.x) {
         const int a = p / F, f = p - a * F;
         const int id = ids[a];
         float val = 0.0f;
@@ -440,8 +463,8 @@ __host__ __device__ inline size_t obs_stage_floats(const GameParams& gp, int g, 
 __device__ __forceinline__ void obs_prologue(const GameParams& gp, const ObsSmem& sm, int g) {
     const TypeParams& T = gp.type[g];
     const int NV = T.view_w * T.view_h;
-    for (int i = threadIdx.x; i < NV; i += blockDim.x) sm.mask[i] = T.view_mask[i];
-    if (threadIdx.x < gp.n_groups) sm.type_hp[threadIdx.x] = gp.type[threadIdx.x].hp;
+    for (int i = TID; i < NV; i += blockDim.x) sm.mask[i] = T.view_mask[i];
+    if (TID < gp.n_groups) sm.type_hp[TID] = gp.type[TID].hp;
 }
 
 // grid: (chunks, E).  Chunk c covers agents [c*chunk, (c+1)*chunk) of group g.
@@ -458,14 +481,14 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     const int a_begin = blockIdx.x * chunk;
     if (a_begin >= n) return;
     const int a_end = min(n, a_begin + chunk);
-    if (a_end > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
+    if (a_end > rowcap) { if (TID == 0) set_err(s, 4); return; }
     size_t off = 0;
     ObsSmem sm = carve_obs(smem, gp, g, s.cap, obs_stage_floats(gp, g, kB, blockDim.x), off);
     if (!kB) sm.hpn = nullptr;
     if (cells_in_lds) {
         uint16_t* lc = reinterpret_cast<uint16_t*>(smem + off);
         const int n2 = s.cells_n;
-        for (int i = threadIdx.x; i < n2; i += blockDim.x) lc[i] = v.cells[i];
+        for (int i = TID; i < n2; i += blockDim.x) lc[i] = v.cells[i];
         v.cells = lc;
     }
     obs_prologue(gp, sm, g);
@@ -495,7 +518,7 @@ __device__ __forceinline__ void set_action_group(const GameParams& gp, const Sta
     int base_a = n_atk, base_m = n_mov;
     __syncthreads();
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
-        const int i = i0 + threadIdx.x;
+        const int i = i0 + TID;
         int a = 0, id = 0, is_move = 0, is_atk = 0;
         uint32_t bucket = kBucketBoundary;
         if (i < n) {
@@ -518,9 +541,9 @@ __device__ __forceinline__ void set_action_group(const GameParams& gp, const Sta
         base_m += tot_m;
         base_a += tot_a;
     }
-    if (base_m > acap || base_a > acap) { if (threadIdx.x == 0) set_err(s, 6); }
+    if (base_m > acap || base_a > acap) { if (TID == 0) set_err(s, 6); }
     __syncthreads();
-    if (threadIdx.x == 0) { n_atk = min(base_a, acap); n_mov = min(base_m, acap); }
+    if (TID == 0) { n_atk = min(base_a, acap); n_mov = min(base_m, acap); }
     __syncthreads();
 }
 
@@ -529,7 +552,7 @@ __global__ void __launch_bounds__(256) k_set_action(const GameParams* __restrict
     __shared__ int wave_tot[16];
     const int e = blockIdx.x;
     EnvView v = global_view(s, e, gp->n_groups);
-    if (v.grp_n[g] > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
+    if (v.grp_n[g] > rowcap) { if (TID == 0) set_err(s, 4); return; }
     set_action_group(*gp, s, v, g, actions + (size_t)e * rowcap, s.atk + (size_t)e * s.acap, s.n_atk[e],
                      s.mov + (size_t)e * s.acap, s.n_mov[e], wave_tot, s.acap);
 }
@@ -554,7 +577,7 @@ __device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem
     for (int g = 0; g < gp.n_groups; ++g) {
         const TypeParams& T = gp.type[g];
         SerialType& S = sm.tt[g];
-        const int t = threadIdx.x;
+        const int t = TID;
         if (t < kMaxRangeCount) {
             S.att_dx[t] = T.att_dx[t]; S.att_dy[t] = T.att_dy[t];
             S.move_dx[t] = T.move_dx[t]; S.move_dy[t] = T.move_dy[t];
@@ -634,14 +657,14 @@ __device__ __forceinline__ void do_move_one(const GameParams& gp, const StepSmem
 
 // Everything of GridWorld::step for one env, executed by the whole workgroup.
 // atk/mov/sorted: pending buffers (any address space); sorted has room for n_mov entries.
-__device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
-                         uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
-                         int& done_out) {
+// sm.tt must hold the serial type table (load_serial_types + barrier).
+__device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
+                              uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
+                              int& done_out) {
     const int G = gp.n_groups;
-    load_serial_types(gp, sm);
     __syncthreads();
     // ---- shuffle + attack: one lane (GridWorld.cc:507-558)
-    if (threadIdx.x == 0) {
+    if (TID == 0) {
         uint32_t x = rng;
         for (int i = 0; i < n_atk; ++i) {
             x = minstd_next(x);
@@ -656,7 +679,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
     for (int g = 0; g < G; ++g) {
         const TypeParams& T = gp.type[g];
         const int n = v.grp_n[g];
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        for (int i = TID; i < n; i += blockDim.x) {
             const int id = v.grp_ids[g * v.cap + i];
             const uint32_t m = v.meta[id];
             if (meta_dead(m)) continue;
@@ -684,7 +707,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
         for (int b = 0; b <= gp.n_sep; ++b) {
             const uint32_t want = b < gp.n_sep ? (uint32_t)b : kBucketBoundary;
             for (int i0 = 0; i0 < n_mov; i0 += blockDim.x) {
-                const int i = i0 + threadIdx.x;
+                const int i = i0 + TID;
                 const uint32_t ent = i < n_mov ? mov[i] : 0u;
                 const int f = i < n_mov && (ent & 0xFF) == want;
                 int tot;
@@ -696,7 +719,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
         __syncthreads();
         order = sorted;
     }
-    if (threadIdx.x == 0)
+    if (TID == 0)
         for (int i = 0; i < n_mov; ++i) do_move_one(gp, sm, v, order[i]);
     __syncthreads();
     // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
@@ -705,9 +728,9 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
         const int n = v.grp_n[R.subj_group];
         int obj_recv = 0;
         for (int k = 0; k < R.n_recv; ++k) obj_recv |= R.recv_is_obj[k];
-        if (threadIdx.x == 0) sm.flags[r] = 0;
+        if (TID == 0) sm.flags[r] = 0;
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        for (int i = TID; i < n; i += blockDim.x) {
             const int id = v.grp_ids[R.subj_group * v.cap + i];
             const uint32_t m = v.meta[id];
             const int ob = v.op_obj[id];
@@ -717,7 +740,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
                 if (!R.recv_is_obj[k]) v.next_r[id] += R.val[k];
         }
         __syncthreads();
-        if (obj_recv && threadIdx.x == 0) {       // object receivers: DFS order, one lane
+        if (obj_recv && TID == 0) {       // object receivers: DFS order, one lane
             for (int i = 0; i < n; ++i) {
                 const int id = v.grp_ids[R.subj_group * v.cap + i];
                 const uint32_t m = v.meta[id];
@@ -730,7 +753,7 @@ __device__ void step_env(const GameParams& gp, const State& s, EnvView& v, uint3
         __syncthreads();
     }
     // ---- done (GridWorld.cc:678-693)
-    if (threadIdx.x == 0) {
+    if (TID == 0) {
         int live = 0;
         for (int g = 0; g < G; ++g) live += (v.grp_n[g] - v.grp_dead[g]) > 0;
         int d = live < G;
@@ -767,27 +790,28 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
         uint32_t* latk = reinterpret_cast<uint32_t*>(carve((size_t)n_atk * 4));
         uint32_t* lmov = reinterpret_cast<uint32_t*>(carve((size_t)n_mov * 4));
         uint32_t* lsort = reinterpret_cast<uint32_t*>(carve((size_t)(gp.large_map ? n_mov : 0) * 4));
-        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
-        for (int i = threadIdx.x; i < nid; i += blockDim.x) {
+        for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
+        for (int i = TID; i < nid; i += blockDim.x) {
             v.xy[i] = gv.xy[i]; v.hp[i] = gv.hp[i]; v.next_r[i] = gv.next_r[i];
             v.op_obj[i] = gv.op_obj[i]; v.meta[i] = gv.meta[i];
         }
-        for (int i = threadIdx.x; i < n_atk; i += blockDim.x) latk[i] = atk[i];
-        for (int i = threadIdx.x; i < n_mov; i += blockDim.x) lmov[i] = mov[i];
+        for (int i = TID; i < n_atk; i += blockDim.x) latk[i] = atk[i];
+        for (int i = TID; i < n_mov; i += blockDim.x) lmov[i] = mov[i];
         atk = latk; mov = lmov; sorted = lsort;
         __syncthreads();
     }
     uint32_t rng = s.rng[e];
     int done = 0;
-    step_env(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done);
+    load_serial_types(gp, sm);
+    step_env_core(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done);
     if (lds) {
-        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
-        for (int i = threadIdx.x; i < nid; i += blockDim.x) {
+        for (int i = TID; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
+        for (int i = TID; i < nid; i += blockDim.x) {
             gv.xy[i] = v.xy[i]; gv.hp[i] = v.hp[i]; gv.next_r[i] = v.next_r[i];
             gv.op_obj[i] = v.op_obj[i]; gv.meta[i] = v.meta[i];
         }
     }
-    if (threadIdx.x == 0) {
+    if (TID == 0) {
         s.rng[e] = rng;
         s.n_atk[e] = 0;
         s.n_mov[e] = 0;
@@ -805,7 +829,7 @@ __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v,
         int32_t* ids = v.grp_ids + g * v.cap;
         int base = 0;
         for (int i0 = 0; i0 < n; i0 += blockDim.x) {
-            const int i = i0 + threadIdx.x;
+            const int i = i0 + TID;
             int id = -1, alive = 0;
             if (i < n) { id = ids[i]; alive = !meta_dead(v.meta[id]); }
             int tot;
@@ -822,7 +846,7 @@ __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v,
             base += tot;
             __syncthreads();
         }
-        if (threadIdx.x == 0) { v.grp_n[g] = base; v.grp_dead[g] = 0; v.grp_reward[g] = 0.0f; }
+        if (TID == 0) { v.grp_n[g] = base; v.grp_dead[g] = 0; v.grp_reward[g] = 0.0f; }
         __syncthreads();
     }
 }
@@ -841,11 +865,11 @@ __global__ void __launch_bounds__(256) k_get(const GameParams* __restrict__ gp, 
     const int e = blockIdx.x;
     EnvView v = global_view(s, e, gp->n_groups);
     const int n = v.grp_n[g];
-    if (what == kGetNum) { if (threadIdx.x == 0) reinterpret_cast<int*>(out)[e] = n; return; }
-    if (n > rowcap) { if (threadIdx.x == 0) set_err(s, 4); return; }
+    if (what == kGetNum) { if (TID == 0) reinterpret_cast<int*>(out)[e] = n; return; }
+    if (n > rowcap) { if (TID == 0) set_err(s, 4); return; }
     const int32_t* ids = v.grp_ids + g * v.cap;
     const size_t o = (size_t)e * rowcap;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int i = TID; i < n; i += blockDim.x) {
         const int id = ids[i];
         switch (what) {
             case kGetReward: reinterpret_cast<float*>(out)[o + i] = v.next_r[id] + v.grp_reward[g]; break;
@@ -895,10 +919,10 @@ __device__ __forceinline__ int rush_action(const GameParams& gp, const EnvView& 
 }
 
 __device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-order reduction
-    red[threadIdx.x] = x;
+    red[TID] = x;
     __syncthreads();
     for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        if ((int)TID < w) red[TID] += red[TID + w];
         __syncthreads();
     }
     const float r = red[0];
@@ -906,6 +930,9 @@ __device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-o
     return r;
 }
 
+#ifndef MFX_ROLLOUT_THREADS
+#define MFX_ROLLOUT_THREADS 256
+#endif
 // LDS plan of k_rollout: the env (cells, per-id arrays, group lists) stays resident for the whole
 // launch; one scratch region is shared by the observation phase (minimap, bins, hp/max, staging) and
 // the policy/step phase (actions, histogram, attack/move buffers; the reduction reuses the actions).
@@ -931,41 +958,28 @@ __host__ __device__ inline size_t rollout_scratch_bytes(const GameParams& gp, in
     return obs > stp ? obs : stp;
 }
 
-size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
+// Bytes of the resident env image in LDS: cells, the seven per-id arrays, the group lists.  The
+// same layout is used for the reset image in HBM (RolloutArgs::reset_image).
+__host__ __device__ inline size_t env_image_bytes(int cells_n, int cap, int G) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const int G = gp.n_groups;
-    size_t b = r16((size_t)cells_n * 2);
-    b += 6 * r16((size_t)cap * 4) + r16(cap);             // xy hp next_r last_r last_act op_obj + meta
-    b += r16((size_t)G * cap * 4);                         // grp_ids
-    b += 4 * r16(G * 4);                                   // grp_n grp_dead grp_reward n_before
-    b += rollout_scratch_bytes(gp, cap, acap, 256);
-    return b;
+    return r16((size_t)cells_n * 2) + 6 * r16((size_t)cap * 4) + r16(cap) + r16((size_t)G * cap * 4);
 }
 
-__device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes) {   // 16-B aligned, bytes % 16 == 0
-    uint4* d = reinterpret_cast<uint4*>(dst);
-    const uint4* q = reinterpret_cast<const uint4*>(src);
-    for (size_t i = threadIdx.x; i < (bytes >> 4); i += blockDim.x) d[i] = q[i];
+size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
+    return env_image_bytes(cells_n, cap, gp.n_groups) + rollout_scratch_bytes(gp, cap, acap, MFX_ROLLOUT_THREADS);
 }
 
-#ifndef MFX_ROLLOUT_THREADS
-#define MFX_ROLLOUT_THREADS 256
-#endif
-template <bool kB>
-__global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParams* __restrict__ gpp, State s, RolloutArgs ra) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ StepSmem sm;
-    __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 2 id_counter, 3 episode end, 4 old id_counter
-    __shared__ unsigned long long steps_acc;
-    const GameParams& gp = *gpp;
-    const int e = blockIdx.x, G = gp.n_groups, cap = s.cap, acap = s.acap;
-    EnvView gv = global_view(s, e, G);
-    // ---------------- carve LDS
+size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap) {
+    return env_image_bytes(cells_n, cap, gp.n_groups) + 64;
+}
+
+// Carve the env image out of LDS (or any base) in the layout above.
+__device__ __forceinline__ EnvView carve_env(char* base, int cells_n, int cap, int G) {
     size_t off = 0;
-    auto carve = [&](size_t bytes) { char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+    auto carve = [&](size_t bytes) { char* p = base + off; off += (bytes + 15) & ~(size_t)15; return p; };
     EnvView v;
     v.cap = cap;
-    v.cells = reinterpret_cast<uint16_t*>(carve((size_t)s.cells_n * 2));
+    v.cells = reinterpret_cast<uint16_t*>(carve((size_t)cells_n * 2));
     v.xy = reinterpret_cast<uint32_t*>(carve((size_t)cap * 4));
     v.hp = reinterpret_cast<float*>(carve((size_t)cap * 4));
     v.next_r = reinterpret_cast<float*>(carve((size_t)cap * 4));
@@ -974,27 +988,218 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParam
     v.op_obj = reinterpret_cast<int32_t*>(carve((size_t)cap * 4));
     v.meta = reinterpret_cast<uint8_t*>(carve((size_t)cap));
     v.grp_ids = reinterpret_cast<int32_t*>(carve((size_t)G * cap * 4));
-    v.grp_n = reinterpret_cast<int32_t*>(carve(G * 4));
-    v.grp_dead = reinterpret_cast<int32_t*>(carve(G * 4));
-    v.grp_reward = reinterpret_cast<float*>(carve(G * 4));
-    int32_t* n_before = reinterpret_cast<int32_t*>(carve(G * 4));
-    char* uni = smem + off;                 // scratch shared by the observation and the step phases
-    size_t soff = off;
-    ObsSmem osm = carve_obs(smem, gp, 0, cap, obs_stage_floats(gp, 0, kB, blockDim.x), soff);
-    if (!kB) osm.hpn = nullptr;
-    const RolloutUnion u = rollout_union(gp, cap, acap, blockDim.x);
-    int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
-    int* ahist = reinterpret_cast<int*>(uni + u.ahist);
-    uint32_t* atk = reinterpret_cast<uint32_t*>(uni + u.atk);
-    uint32_t* mov = reinterpret_cast<uint32_t*>(uni + u.mov);
-    uint32_t* sorted = reinterpret_cast<uint32_t*>(uni + u.sorted);
-    float* red = reinterpret_cast<float*>(uni + u.red);
-    MFX_STAMP(0);
-    // ---------------- load the env (whole 16-B rows; cap is a power of two >= 64)
+    return v;
+}
+
+__device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes) {   // 16-B aligned, bytes % 16 == 0
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const uint4* q = reinterpret_cast<const uint4*>(src);
+    for (size_t i = TID; i < (bytes >> 4); i += blockDim.x) d[i] = q[i];
+}
+
+// env.reset() + add_agents(custom) of the template (GridWorld.cc:76-124, Map.cc:23-47, 200-247),
+// computed once per rollout_init by one workgroup; k_rollout copies it in at every episode start.
+__global__ void __launch_bounds__(256) k_reset_image(const GameParams* __restrict__ gpp, int cells_n, int cap,
+                                                     RolloutArgs ra, uint4* __restrict__ image) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int scal[8];
+    const GameParams& gp = *gpp;
+    const int G = gp.n_groups, W = gp.W, H = gp.H;
+    EnvView v = carve_env(smem, cells_n, cap, G);
+    const size_t bytes = env_image_bytes(cells_n, cap, G);
+    for (size_t i = TID; i < bytes / 4; i += blockDim.x) reinterpret_cast<uint32_t*>(smem)[i] = 0;
+    __syncthreads();
+    for (int c = TID; c < W * H; c += blockDim.x) {
+        const int x = c % W, y = c / W;
+        v.cells[c] = (x == 0 || y == 0 || x == W - 1 || y == H - 1) ? kCellWall : kCellEmpty;
+    }
+    __syncthreads();
+    if (TID == 0) {
+        int idc = 0;
+        for (int g = 0; g < kMaxGroups; ++g) scal[g] = 0;
+        for (int g = 0; g < G; ++g) {
+            const TypeParams& T = gp.type[g];
+            for (int i = 0; i < ra.tmpl_n[g]; ++i) {
+                const int x = ra.tmpl_x[g * ra.tmpl_cap + i], y = ra.tmpl_y[g * ra.tmpl_cap + i];
+                if (!is_blank(v.cells, W, H, x, y, -1) || idc >= cap) continue;
+                const int id = idc++;
+                v.cells[y * W + x] = (uint16_t)id;
+                v.xy[id] = (uint32_t)x | ((uint32_t)y << 16);
+                v.hp[id] = T.hp; v.last_r[id] = 0.0f; v.next_r[id] = T.step_reward;
+                v.last_act[id] = T.n_action; v.op_obj[id] = -1;
+                v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
+                v.grp_ids[g * cap + scal[g]++] = id;
+            }
+        }
+        scal[4] = idc;
+        for (int k = 5; k < 8; ++k) scal[k] = 0;
+    }
+    __syncthreads();
+    copy16(image, smem, bytes);
+    if (TID < 8) reinterpret_cast<int32_t*>(reinterpret_cast<char*>(image) + bytes)[TID] = scal[TID];
+}
+
+// Per-env scalars of k_rollout, held in LDS while the env is resident.  Word w of this struct is
+// loaded / stored by lane w (addresses from PfTable).
+struct EnvScalars {
+    int32_t grp_n[kMaxGroups];          // words 0-3
+    int32_t grp_dead[kMaxGroups];       // 4-7
+    float grp_reward[kMaxGroups];       // 8-11
+    float ep_return[kMaxGroups];        // 12-15
+    int32_t id_counter;                 // 16
+    uint32_t rng;                       // 17
+    int32_t ep_len;                     // 18
+    int32_t pad;                        // 19
+    double stats[4];                    // 20-27
+    unsigned long long agent_steps;     // 28-29
+};
+constexpr int kScalarWords = 30;
+
+// Register prefetch of one env (k_rollout fast path): while env e is processed, every lane of
+// waves 0-2 holds its share of env e+1's image (3 + 3 rows of 16 B; wave 0 also one scalar word),
+// so the next install is LDS stores only.  Wave 3 alone writes env e back: a wave's vmcnt is in
+// order, so the prefetch waves must not have the write-back stores queued ahead of their loads.
+// The 16-B rows of the per-id arrays and group lists are numbered in LDS order:
+// [xy hp next_r last_r last_act op_obj] (c4 = cap/4 rows each), [meta] (c4/4), [grp_ids] (G*c4).
+constexpr int kPfLanes = 192;                     // waves 0-2
+constexpr int kPfCellRows = 3 * kPfLanes;
+constexpr int kPfSmallRows = 3 * kPfLanes;
+constexpr int kWbWave = 3;                        // the write-back wave
+
+struct EnvPrefetch {
+    uint4 c0, c1, c2, a0, a1, a2;
+    uint32_t w;
+};
+
+// Address plan of the env image, built once per workgroup in LDS: for each source array (the six
+// 4-byte per-id arrays, meta, grp_ids) and each EnvScalars word, the env-0 address and the bytes
+// per env.  A prefetch row is then ONE load from base + e * stride + offset; choosing among
+// separate pointers per lane instead would serialise the loads (each predicated load into the same
+// registers waits for the previous one).
+struct PfTable {
+    unsigned long long base[8];
+    unsigned int stride[8];
+    unsigned long long sbase[32];       // 0: word absent (group >= G, padding)
+    unsigned int sstride[32];
+};
+
+__device__ __forceinline__ void pf_table_init(PfTable& pt, const State& s, const RolloutArgs& ra, int G) {
+    const int t = TID;
+    const unsigned cap4 = (unsigned)s.cap * 4u;
+    if (t < 8) {
+        const void* p = nullptr;
+        unsigned st = cap4;
+        if (t == 0) p = s.xy;
+        if (t == 1) p = s.hp;
+        if (t == 2) p = s.next_r;
+        if (t == 3) p = s.last_r;
+        if (t == 4) p = s.last_act;
+        if (t == 5) p = s.op_obj;
+        if (t == 6) { p = s.meta; st = (unsigned)s.cap; }
+        if (t == 7) { p = s.grp_ids; st = cap4 * (unsigned)G; }
+        pt.base[t] = (unsigned long long)p;
+        pt.stride[t] = st;
+    }
+    if (t < 32) {
+        const int g = t & 3;
+        const char* p = nullptr;
+        unsigned st = 4;
+        if (t < 16 && g < G) {
+            st = 4u * (unsigned)G;
+            if ((t >> 2) == 0) p = reinterpret_cast<const char*>(s.grp_n + g);
+            if ((t >> 2) == 1) p = reinterpret_cast<const char*>(s.grp_dead + g);
+            if ((t >> 2) == 2) p = reinterpret_cast<const char*>(s.grp_reward + g);
+            if ((t >> 2) == 3) p = reinterpret_cast<const char*>(ra.ep_return + g);
+        }
+        if (t == 16) p = reinterpret_cast<const char*>(s.id_counter);
+        if (t == 17) p = reinterpret_cast<const char*>(s.rng);
+        if (t == 18) p = reinterpret_cast<const char*>(ra.ep_len);
+        if (t >= 20 && t < 28) { p = reinterpret_cast<const char*>(ra.stats) + 4 * (t - 20); st = 32; }
+        if (t >= 28 && t < 30) { p = reinterpret_cast<const char*>(ra.agent_steps) + 4 * (t - 28); st = 8; }
+        pt.sbase[t] = (unsigned long long)p;
+        pt.sstride[t] = st;
+    }
+}
+
+// Table addresses are integers: cast them to the GLOBAL address space.  A generic pointer would
+// make these flat_load / flat_store, which also count in lgkmcnt, so every later LDS wait would
+// wait for the HBM round trip too.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+
+__device__ __forceinline__ uint4 ld_g16(const g_u32x4* p) {
+    const u32x4 x = *p;
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// Address of 16-B row k of the small region of env e (LDS order, see EnvPrefetch).
+__device__ __forceinline__ const g_u32x4* small_row_addr(const PfTable& pt, int e, int k, int sh, int c4) {
+    const int j = k >> sh, k2 = k - 6 * c4, mrows = c4 >> 2;
+    const int a = j < 6 ? j : (k2 < mrows ? 6 : 7);
+    const int r = j < 6 ? (k & (c4 - 1)) : (k2 < mrows ? k2 : k2 - mrows);
+    return (const g_u32x4*)(pt.base[a] + (unsigned long long)e * pt.stride[a] + (unsigned)r * 16u);
+}
+
+__device__ __forceinline__ g_u32* scalar_addr(const PfTable& pt, int e, int w) {
+    const unsigned long long b = pt.sbase[w];
+    return b ? (g_u32*)(b + (unsigned long long)e * pt.sstride[w]) : nullptr;
+}
+
+__device__ __forceinline__ uint32_t load_scalar_word(const PfTable& pt, int e, int w) {
+    const g_u32* p = scalar_addr(pt, e, w);
+    return p ? *p : 0u;
+}
+
+__device__ __forceinline__ void pf_issue(EnvPrefetch& pf, const PfTable& pt, const State& s, int e, int nc16,
+                                         int ns16, int sh, int c4) {
+    const int t = TID;
+    if (t >= kPfLanes) return;
+    const uint4* gc = reinterpret_cast<const uint4*>(s.cells + (size_t)e * s.cells_n);
+    if (t < nc16) pf.c0 = gc[t];
+    if (t + kPfLanes < nc16) pf.c1 = gc[t + kPfLanes];
+    if (t + 2 * kPfLanes < nc16) pf.c2 = gc[t + 2 * kPfLanes];
+    if (t < ns16) pf.a0 = ld_g16(small_row_addr(pt, e, t, sh, c4));
+    if (t + kPfLanes < ns16) pf.a1 = ld_g16(small_row_addr(pt, e, t + kPfLanes, sh, c4));
+    if (t + 2 * kPfLanes < ns16) pf.a2 = ld_g16(small_row_addr(pt, e, t + 2 * kPfLanes, sh, c4));
+    if (t < kScalarWords) pf.w = load_scalar_word(pt, e, t);
+}
+
+__device__ __forceinline__ void pf_install(const EnvPrefetch& pf, const EnvView& v, EnvScalars& sc, int nc16,
+                                           int ns16) {
+    // One unconditional vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  Left to the
+    // compiler, the waits sit inside the exec-masked stores below, so along the skipped paths the
+    // registers still look in flight and the next pf_issue waits again before every load.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    const int t = TID;
+    if (t >= kPfLanes) return;
+    uint4* lc = reinterpret_cast<uint4*>(v.cells);
+    uint4* la = reinterpret_cast<uint4*>(v.xy);
+    if (t < nc16) lc[t] = pf.c0;
+    if (t + kPfLanes < nc16) lc[t + kPfLanes] = pf.c1;
+    if (t + 2 * kPfLanes < nc16) lc[t + 2 * kPfLanes] = pf.c2;
+    if (t < ns16) la[t] = pf.a0;
+    if (t + kPfLanes < ns16) la[t + kPfLanes] = pf.a1;
+    if (t + 2 * kPfLanes < ns16) la[t + 2 * kPfLanes] = pf.a2;
+    if (t < kScalarWords) reinterpret_cast<uint32_t*>(&sc)[t] = pf.w;
+}
+
+// 16-B copy by one wave (lane stride 64).
+__device__ __forceinline__ void wcopy16(void* dst, const void* src, size_t bytes, int lane) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const uint4* q = reinterpret_cast<const uint4*>(src);
+    for (size_t i = lane; i < (bytes >> 4); i += 64) d[i] = q[i];
+}
+
+// Generic install (maps / capacities beyond the prefetch budget): straight copies.
+__device__ __forceinline__ void install_sync(const State& s, const PfTable& pt, int e, int G, const EnvView& v,
+                                             EnvScalars& sc) {
+    const EnvView gv = global_view(s, e, G);
+    const int cap = s.cap;
     if ((s.cells_n & 7) == 0) {
         copy16(v.cells, gv.cells, (size_t)s.cells_n * 2);
     } else {
-        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
+        for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
     }
     copy16(v.xy, gv.xy, (size_t)cap * 4);
     copy16(v.hp, gv.hp, (size_t)cap * 4);
@@ -1004,170 +1209,232 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS) k_rollout(const GameParam
     copy16(v.op_obj, gv.op_obj, (size_t)cap * 4);
     copy16(v.meta, gv.meta, (size_t)cap);
     copy16(v.grp_ids, gv.grp_ids, (size_t)G * cap * 4);
-    if (threadIdx.x < G) {
-        const int n = gv.grp_n[threadIdx.x];
-        v.grp_n[threadIdx.x] = n;
-        n_before[threadIdx.x] = n;
-        v.grp_dead[threadIdx.x] = gv.grp_dead[threadIdx.x];
-        v.grp_reward[threadIdx.x] = gv.grp_reward[threadIdx.x];
-    }
-    if (threadIdx.x == 0) {
-        misc[0] = 0; misc[1] = 0;
-        misc[4] = s.id_counter[e];
-        steps_acc = ra.agent_steps[e];
-    }
-    __syncthreads();
-    MFX_STAMP(1);
-    // ---------------- get_observation for every group
-    obs_prologue(gp, osm, 0);
-    obs_minimap<kB>(gp, v, osm);
-    MFX_STAMP(2);
-    for (int g = 0; g < G; ++g) {
-        const TypeParams& T = gp.type[g];
-        const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
-        float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
-        float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
-        const int n = min(v.grp_n[g], ra.rowcap);
-        if (kB) {
-            obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
-        } else {
-            obs_prologue(gp, osm, g);
-            __syncthreads();
-            for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
-        }
-    }
-    __syncthreads();                       // the scratch region changes hands
-    MFX_STAMP(3);
-    // ---------------- policy + mean action (former_act_prob), all groups in one pass
+    if (TID < kScalarWords)
+        reinterpret_cast<uint32_t*>(&sc)[TID] = load_scalar_word(pt, e, TID);
+}
+
+// One launch = one training-loop step for every env.  Persistent workgroups: the grid is what
+// fits on the chip at once, and each workgroup takes envs from a work queue, keeping env e in LDS
+// while the next env's image is already in flight into registers.
+template <bool kB, bool kPf>
+__global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GameParams* __restrict__ gpp,
+                                                                 const RolloutCtx* __restrict__ ctx,
+                                                                 uint32_t step_index, int work_sel) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ StepSmem sm;
+    __shared__ EnvScalars sc;
+    __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 3 episode end, 4 done, 5-7 queue hand-off
+    __shared__ int32_t n_before[kMaxGroups];
+    __shared__ PfTable pt;
+    // Work queue: position i of this launch is env ra.order[i] (heaviest envs first, k_env_order).
+    // The hand-off is pipelined so that no queue access is waited on: while env e_k is processed,
+    // e_{k+1} is being prefetched, thread 0 holds e_{k+2} (o) and the queue slot of e_{k+3} (g),
+    // and both loads land before the next install's vmcnt(0).
+    int e, en;
+    int o = 0, g = 0;
+    EnvPrefetch pf;
+    pf.c0 = pf.c1 = pf.c2 = pf.a0 = pf.a1 = pf.a2 = make_uint4(0, 0, 0, 0);
+    pf.w = 0;
     {
-        int ntot = 0;
-        for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
-        for (int i = threadIdx.x; i < G * 64; i += blockDim.x) ahist[i] = 0;
-        __syncthreads();
-        for (int t = threadIdx.x; t < ntot; t += blockDim.x) {
-            int g = 0, i = t;
-            while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
-            const int id = v.grp_ids[g * cap + i];
-            const uint32_t key = ra.policy_seed ^ mix32(ra.step_index * 0x9E3779B9u + (uint32_t)e * 0x632BE5ABu) ^
-                                 mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
-            const int a = rush_action(gp, v, g, id, key, ra.eps);
-            act[g * cap + i] = a;
-            if (i < ra.rowcap) ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
-            atomicAdd(&ahist[g * 64 + a], 1);
-        }
-        __syncthreads();
-        for (int t = threadIdx.x; t < G * 64; t += blockDim.x) {
-            const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
-            if (k < na)   // empty group: np.mean of nothing is NaN
-                ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
-        }
-    }
-    MFX_STAMP(4);
-    // ---------------- set_action (group order) and step
-    for (int g = 0; g < G; ++g) set_action_group(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
-    MFX_STAMP(5);
-    uint32_t rng = s.rng[e];
-    int done = 0;
-    step_env(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done);
-    MFX_STAMP(6);
-    // ---------------- get_reward, episode return, kills
-    float kills = 0.0f;
-    for (int g = 0; g < G; ++g) {
-        const int n = v.grp_n[g];
-        float part = 0.0f;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const float r = v.next_r[v.grp_ids[g * cap + i]] + v.grp_reward[g];
-            if (i < ra.rowcap) ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
-            part += r;
-        }
-        const float tot = block_sum(part, red);
-        if (threadIdx.x == 0) { ra.ep_return[e * G + g] += tot; kills += (float)v.grp_dead[g]; }
-    }
-    MFX_STAMP(7);
-    // ---------------- clear_dead
-    clear_dead_env(gp, v, sm.wave_tot);
-    MFX_STAMP(8);
-    // ---------------- episode end -> reset + re-place the template (env.reset + add_agents)
-    if (threadIdx.x == 0) {
-        double* st = ra.stats + (size_t)e * 4;
-        st[3] += kills;
-        int len = ra.ep_len[e] + 1;
-        if (done || len >= ra.max_steps) {
-            st[0] += 1.0;
-            st[1] += ra.ep_return[e * G + 0];
-            st[2] += G > 1 ? ra.ep_return[e * G + 1] : 0.0f;
-            for (int g = 0; g < G; ++g) ra.ep_return[e * G + g] = 0.0f;
-            len = 0;
-            misc[3] = 1;
-        } else {
-            misc[3] = 0;
-        }
-        ra.ep_len[e] = len;
-        s.rng[e] = rng;
-        s.done[e] = done;
-    }
-    __syncthreads();
-    int id_counter = misc[4];
-    if (misc[3]) {
-        const int W = gp.W, H = gp.H;
-        for (int c = threadIdx.x; c < W * H; c += blockDim.x) {
-            const int x = c % W, y = c / W;
-            v.cells[c] = (x == 0 || y == 0 || x == W - 1 || y == H - 1) ? kCellWall : kCellEmpty;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int idc = 0;
-            for (int g = 0; g < G; ++g) {
-                const TypeParams& T = gp.type[g];
-                v.grp_n[g] = 0; v.grp_dead[g] = 0; v.grp_reward[g] = 0.0f;
-                for (int i = 0; i < ra.tmpl_n[g]; ++i) {
-                    const int x = ra.tmpl_x[g * ra.tmpl_cap + i], y = ra.tmpl_y[g * ra.tmpl_cap + i];
-                    if (!is_blank(v.cells, W, H, x, y, -1) || idc >= cap) continue;
-                    const int id = idc++;
-                    v.cells[y * W + x] = (uint16_t)id;
-                    v.xy[id] = (uint32_t)x | ((uint32_t)y << 16);
-                    v.hp[id] = T.hp; v.last_r[id] = 0.0f; v.next_r[id] = T.step_reward;
-                    v.last_act[id] = T.n_action; v.op_obj[id] = -1;
-                    v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
-                    v.grp_ids[g * cap + v.grp_n[g]++] = id;
-                }
+        const GameParams& gp = kconst(gpp);
+        const State& s = kconst(ctx).s;
+        const RolloutArgs& ra = kconst(ctx).ra;
+        const int G = gp.n_groups, c4 = s.cap >> 2, sh = __ffs(c4) - 1;
+        const int nc16 = s.cells_n >> 3, ns16 = 6 * c4 + (c4 >> 2) + G * c4;
+        if (TID == 0) {
+            if (blockIdx.x == 0) ra.work[work_sel ^ 1] = 0;
+            for (int k = 5; k < 8; ++k) {
+                const int i = atomicAdd(ra.work + work_sel, 1);
+                misc[k] = i < s.E ? ra.order[i] : s.E;
             }
-            misc[2] = idc;
+            g = atomicAdd(ra.work + work_sel, 1);
+        }
+        load_serial_types(gp, sm);
+        pf_table_init(pt, s, ra, G);
+        __syncthreads();
+        e = misc[5]; en = misc[6];
+        if (TID == 0) o = misc[7];
+        if (kPf && e < s.E) pf_issue(pf, pt, s, e, nc16, ns16, sh, c4);
+    }
+    while (true) {
+#ifdef MFX_STAMPS
+    if (TID == 0 && g_stamps && e < kconst(ctx).s.E) g_stamps[e * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+#endif
+    // every iteration re-reads its parameters through scalar loads (see RolloutCtx)
+    const GameParams& gp = kconst(gpp);
+    const State& s = kconst(ctx).s;
+    const RolloutArgs& ra = kconst(ctx).ra;
+    if (e >= s.E) break;
+    const int G = gp.n_groups, cap = s.cap, acap = s.acap;
+    // ---------------- carve LDS
+    EnvView v = carve_env(smem, s.cells_n, cap, G);
+    v.grp_n = sc.grp_n; v.grp_dead = sc.grp_dead; v.grp_reward = sc.grp_reward;
+    const size_t soff = env_image_bytes(s.cells_n, cap, G);
+    char* uni = smem + soff;                 // scratch shared by the observation and the step phases
+    size_t soff2 = soff;
+    ObsSmem osm = carve_obs(smem, gp, 0, cap, obs_stage_floats(gp, 0, kB, blockDim.x), soff2);
+    if (!kB) osm.hpn = nullptr;
+    const RolloutUnion u = rollout_union(gp, cap, acap, blockDim.x);
+    int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
+    int* ahist = reinterpret_cast<int*>(uni + u.ahist);
+    uint32_t* atk = reinterpret_cast<uint32_t*>(uni + u.atk);
+    uint32_t* mov = reinterpret_cast<uint32_t*>(uni + u.mov);
+    uint32_t* sorted = reinterpret_cast<uint32_t*>(uni + u.sorted);
+    float* red = reinterpret_cast<float*>(uni + u.red);
+    const size_t img_bytes = env_image_bytes(s.cells_n, cap, G);
+    const int32_t* img_scal = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(ra.reset_image) + img_bytes);
+    const int c4 = cap >> 2, sh = __ffs(c4) - 1;
+    const int nc16 = s.cells_n >> 3, ns16 = 6 * c4 + (c4 >> 2) + G * c4;
+    {
+        const int stamp_row = e;
+        (void)stamp_row;
+        MFX_STAMP(0);
+        // ---------------- install env e
+        if (kPf) pf_install(pf, v, sc, nc16, ns16);
+        else install_sync(s, pt, e, G, v, sc);
+        if (TID == 0) { misc[0] = 0; misc[1] = 0; misc[5] = o; }
+        __syncthreads();
+        MFX_STAMP(13);
+        if (TID < G) n_before[TID] = sc.grp_n[TID];
+        if (kPf && en < s.E) pf_issue(pf, pt, s, en, nc16, ns16, sh, c4);
+        if (TID == 0) {                        // lands long before the next install
+            o = g < s.E ? ra.order[g] : s.E;
+            g = atomicAdd(ra.work + work_sel, 1);
+        }
+        MFX_STAMP(1);
+        // ---------------- get_observation for every group
+        obs_prologue(gp, osm, 0);
+        obs_minimap<kB>(gp, v, osm);
+        MFX_STAMP(2);
+        for (int g = 0; g < G; ++g) {
+            const TypeParams& T = gp.type[g];
+            const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
+            float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
+            float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
+            const int n = min(v.grp_n[g], ra.rowcap);
+            if (kB) {
+                obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
+            } else {
+                obs_prologue(gp, osm, g);
+                __syncthreads();
+                for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
+            }
+        }
+        __syncthreads();                       // the scratch region changes hands
+        MFX_STAMP(3);
+        // ---------------- policy + mean action (former_act_prob), all groups in one pass
+        {
+            int ntot = 0;
+            for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+            for (int i = TID; i < G * 64; i += blockDim.x) ahist[i] = 0;
+            __syncthreads();
+            const uint32_t ekey = ra.policy_seed ^ mix32(step_index * 0x9E3779B9u + (uint32_t)e * 0x632BE5ABu);
+            for (int t = TID; t < ntot; t += blockDim.x) {
+                int g = 0, i = t;
+                while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
+                const int id = v.grp_ids[g * cap + i];
+                const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
+                const int a = rush_action(gp, v, g, id, key, ra.eps);
+                act[g * cap + i] = a;
+                if (i < ra.rowcap) ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
+                atomicAdd(&ahist[g * 64 + a], 1);
+            }
+            __syncthreads();
+            for (int t = TID; t < G * 64; t += blockDim.x) {
+                const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
+                if (k < na)   // empty group: np.mean of nothing is NaN
+                    ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
+            }
+        }
+        MFX_STAMP(4);
+        // ---------------- set_action (group order) and step
+        for (int g = 0; g < G; ++g) set_action_group(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
+        MFX_STAMP(5);
+        uint32_t rng = sc.rng;
+        int done = 0;
+        step_env_core(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done);
+        MFX_STAMP(6);
+        // ---------------- get_reward, episode return, kills
+        float kills = 0.0f;
+        for (int g = 0; g < G; ++g) {
+            const int n = v.grp_n[g];
+            float part = 0.0f;
+            for (int i = TID; i < n; i += blockDim.x) {
+                const float r = v.next_r[v.grp_ids[g * cap + i]] + v.grp_reward[g];
+                if (i < ra.rowcap) ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
+                part += r;
+            }
+            const float tot = block_sum(part, red);
+            if (TID == 0) { sc.ep_return[g] += tot; kills += (float)v.grp_dead[g]; }
+        }
+        MFX_STAMP(7);
+        // ---------------- clear_dead
+        clear_dead_env(gp, v, sm.wave_tot);
+        MFX_STAMP(8);
+        // ---------------- episode end -> reset + re-place the template (env.reset + add_agents)
+        if (TID == 0) {
+            sc.stats[3] += kills;
+            int len = sc.ep_len + 1;
+            misc[3] = 0;
+            if (done || len >= ra.max_steps) {
+                sc.stats[0] += 1.0;
+                sc.stats[1] += sc.ep_return[0];
+                sc.stats[2] += G > 1 ? sc.ep_return[1] : 0.0f;
+                for (int g = 0; g < G; ++g) sc.ep_return[g] = 0.0f;
+                len = 0;
+                misc[3] = 1;
+            }
+            sc.ep_len = len;
+            sc.rng = rng;
+            misc[4] = done;
+            unsigned long long tot = 0;
+            for (int g = 0; g < G; ++g) tot += (unsigned)n_before[g];
+            sc.agent_steps += tot;
         }
         __syncthreads();
-        id_counter = misc[2];
+        if (misc[3]) {
+            copy16(v.cells, ra.reset_image, img_bytes);
+            if (TID < G) {
+                sc.grp_n[TID] = img_scal[TID];
+                sc.grp_dead[TID] = 0;
+                sc.grp_reward[TID] = 0.0f;
+            }
+            if (TID == 0) sc.id_counter = img_scal[4];
+            __syncthreads();
+        }
+        MFX_STAMP(9);
+        // ---------------- write the env back (wave kWbWave only, see EnvPrefetch)
+        if ((TID >> 6) == kWbWave) {
+            const int lane = TID & 63;
+            const EnvView gv = global_view(s, e, G);
+            if ((s.cells_n & 7) == 0) {
+                wcopy16(gv.cells, v.cells, (size_t)s.cells_n * 2, lane);
+            } else {
+                for (int i = lane; i < s.cells_n; i += 64) gv.cells[i] = v.cells[i];
+            }
+            const int idc = sc.id_counter;
+            const size_t n4 = ((size_t)idc + 3) & ~(size_t)3, n16 = ((size_t)idc + 15) & ~(size_t)15;
+            wcopy16(gv.xy, v.xy, n4 * 4, lane);
+            wcopy16(gv.hp, v.hp, n4 * 4, lane);
+            wcopy16(gv.next_r, v.next_r, n4 * 4, lane);
+            wcopy16(gv.last_r, v.last_r, n4 * 4, lane);
+            wcopy16(gv.last_act, v.last_act, n4 * 4, lane);
+            wcopy16(gv.op_obj, v.op_obj, n4 * 4, lane);
+            wcopy16(gv.meta, v.meta, n16, lane);
+            for (int g = 0; g < G; ++g)
+                wcopy16(gv.grp_ids + g * cap, v.grp_ids + g * cap, (((size_t)v.grp_n[g] + 3) & ~(size_t)3) * 4, lane);
+            if (lane < kScalarWords) {
+                g_u32* p = scalar_addr(pt, e, lane);
+                if (p) *p = reinterpret_cast<const uint32_t*>(&sc)[lane];
+            }
+            if (lane == 0) { s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = misc[4]; }
+        }
+        MFX_STAMP(10);
+        __syncthreads();                       // LDS reads of the write-back are done; hand-off visible
+        e = en;
+        en = misc[5];
     }
-    MFX_STAMP(9);
-    // ---------------- write the env back
-    if ((s.cells_n & 7) == 0) {
-        copy16(gv.cells, v.cells, (size_t)s.cells_n * 2);
-    } else {
-        for (int i = threadIdx.x; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
     }
-    {
-        const size_t n4 = ((size_t)id_counter + 3) & ~(size_t)3, n16 = ((size_t)id_counter + 15) & ~(size_t)15;
-        copy16(gv.xy, v.xy, n4 * 4);
-        copy16(gv.hp, v.hp, n4 * 4);
-        copy16(gv.next_r, v.next_r, n4 * 4);
-        copy16(gv.last_r, v.last_r, n4 * 4);
-        copy16(gv.last_act, v.last_act, n4 * 4);
-        copy16(gv.op_obj, v.op_obj, n4 * 4);
-        copy16(gv.meta, v.meta, n16);
-        for (int g = 0; g < G; ++g)
-            copy16(gv.grp_ids + g * cap, v.grp_ids + g * cap, (((size_t)v.grp_n[g] + 3) & ~(size_t)3) * 4);
-    }
-    if (threadIdx.x < G) {
-        gv.grp_n[threadIdx.x] = v.grp_n[threadIdx.x];
-        gv.grp_dead[threadIdx.x] = v.grp_dead[threadIdx.x];
-        gv.grp_reward[threadIdx.x] = v.grp_reward[threadIdx.x];
-    }
-    if (threadIdx.x == 0) {
-        unsigned long long tot = 0;
-        for (int g = 0; g < G; ++g) tot += (unsigned)n_before[g];
-        ra.agent_steps[e] = steps_acc + tot;
-        s.id_counter[e] = id_counter; s.n_atk[e] = 0; s.n_mov[e] = 0;
-    }
-    MFX_STAMP(10);
 }
 
 // ==================================================================================
@@ -1239,14 +1506,89 @@ hipError_t set_stamp_buffer(unsigned long long* d_buf) {
 #endif
 }
 
-hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
-                          hipStream_t st) {
+// The register-prefetch instance needs the env image to fit the prefetch lanes (see EnvPrefetch).
+static bool rollout_prefetch_ok(const GameParams& gp, const State& s) {
+    const int c4 = s.cap >> 2, nc16 = s.cells_n >> 3, ns16 = 6 * c4 + (c4 >> 2) + gp.n_groups * c4;
+    return (s.cells_n & 7) == 0 && nc16 <= kPfCellRows && ns16 <= kPfSmallRows;
+}
+
+template <class F>
+static hipError_t with_rollout_kernel(const GameParams& gp, const State& s, F&& f) {
+    if (is_battle_shape(gp)) {
+        if (rollout_prefetch_ok(gp, s)) return f(k_rollout<true, true>);
+        return f(k_rollout<true, false>);
+    }
+    return f(k_rollout<false, false>);
+}
+
+hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                          uint32_t step_index, int work_sel, int grid, hipStream_t st) {
     const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
-    if (is_battle_shape(gp))
-        k_rollout<true><<<s.E, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, s, ra);
-    else
-        k_rollout<false><<<s.E, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, s, ra);
+    return with_rollout_kernel(gp, s, [&](auto kern) {
+        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel);
+        return hipGetLastError();
+    });
+}
+
+// Persistent grid of k_rollout: every workgroup that can be resident at once (more is harmless --
+// the extra ones find the queue empty -- fewer would idle CUs).
+hipError_t rollout_grid(const GameParams& gp, const State& s, int* grid) {
+    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (err != hipSuccess) return err;
+    err = with_rollout_kernel(gp, s, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, MFX_ROLLOUT_THREADS, smem);
+    });
+    if (err != hipSuccess) return err;
+    const long long want = (long long)cus * (per_cu > 0 ? per_cu : 1);
+    *grid = (int)(want < s.E ? want : s.E);
+    return hipSuccess;
+}
+
+// Queue order of the next k_rollout launch: env indices by descending agent count (the cost of an
+// env's step grows with it), so the heaviest envs start first and the launch does not end on a
+// tail of a few late episode starts.  One workgroup; counting sort over the agent count.
+constexpr int kOrderBuckets = 1024;
+
+__global__ void __launch_bounds__(1024) k_env_order(const int32_t* __restrict__ grp_n, int E, int G,
+                                                    int32_t* __restrict__ order) {
+    __shared__ int off[kOrderBuckets];
+    const int t = TID;
+    off[t] = 0;
+    __syncthreads();
+    auto bucket = [&](int e) {
+        int w = 0;
+        for (int k = 0; k < G; ++k) w += grp_n[e * G + k];
+        return kOrderBuckets - 1 - min(max(w, 0), kOrderBuckets - 1);
+    };
+    for (int e = t; e < E; e += 1024) atomicAdd(&off[bucket(e)], 1);
+    __syncthreads();
+    for (int d = 1; d < kOrderBuckets; d <<= 1) {     // inclusive scan
+        const int x = t >= d ? off[t - d] : 0;
+        __syncthreads();
+        off[t] += x;
+        __syncthreads();
+    }
+    const int excl = t ? off[t - 1] : 0;
+    __syncthreads();
+    off[t] = excl;
+    __syncthreads();
+    for (int e = t; e < E; e += 1024) order[atomicAdd(&off[bucket(e)], 1)] = e;
+}
+
+hipError_t launch_env_order(const State& s, int G, int32_t* d_order, hipStream_t st) {
+    k_env_order<<<1, 1024, 0, st>>>(s.grp_n, s.E, G, d_order);
+    return hipGetLastError();
+}
+
+hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
+                              uint4* d_image, hipStream_t st) {
+    const size_t smem = env_image_bytes(s.cells_n, s.cap, gp.n_groups);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    k_reset_image<<<1, 256, smem, st>>>(d_gp, s.cells_n, s.cap, ra, d_image);
     return hipGetLastError();
 }
 

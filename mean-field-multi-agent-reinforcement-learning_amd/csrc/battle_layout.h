@@ -117,6 +117,18 @@ struct RolloutArgs {
     uint32_t policy_seed;
     uint32_t step_index;            // global step counter (policy RNG stream)
     float eps;                      // random-action probability of the rush policy
+    const int32_t* order;           // [E] queue order of the launch (k_env_order)
+    int32_t* work;                  // [2] env work-queue counters; launch k uses work[k & 1]
+    int work_sel;                   //     and zeroes the other one for launch k + 1
+    const uint4* reset_image;       // LDS image of the env right after reset + template placement,
+                                    // followed by int32 [grp_n[kMaxGroups], id_counter]
+};
+
+// Everything k_rollout reads besides GameParams, resident in HBM (uploaded when it changes); the
+// kernel re-reads it per env through scalar loads instead of pinning ~80 SGPRs for the launch.
+struct RolloutCtx {
+    State s;
+    RolloutArgs ra;
 };
 
 // meta helpers

@@ -31,7 +31,7 @@ class BattleBatch:
                    "mfx_battle_set_action", "mfx_battle_step", "mfx_battle_get", "mfx_battle_clear_dead",
                    "mfx_battle_sync", "mfx_battle_rollout_init", "mfx_battle_rollout_step",
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
-                   "mfx_battle_group_capacity"):
+                   "mfx_battle_rollout_info", "mfx_battle_group_capacity"):
             getattr(self._dll, fn).restype = ctypes.c_int
         self._dll.mfx_last_error.restype = ctypes.c_char_p
         self.handles = self.env.get_handles()
@@ -104,6 +104,12 @@ class BattleBatch:
         rc = ctypes.c_int()
         self._dll.mfx_battle_rollout_rowcap(self.game, ctypes.byref(rc))
         self.rowcap = rc.value
+
+    def rollout_info(self):
+        """(persistent grid in workgroups, dynamic LDS bytes per workgroup) of the fused rollout."""
+        g, b = ctypes.c_int(), ctypes.c_int()
+        self._check(self._dll.mfx_battle_rollout_info(self.game, ctypes.byref(g), ctypes.byref(b)), "rollout_info")
+        return g.value, b.value
 
     def rollout_step(self, n_steps=1):
         self._check(self._dll.mfx_battle_rollout_step(self.game, n_steps), "rollout_step")

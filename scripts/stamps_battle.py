@@ -20,23 +20,40 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--envs", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=5)
 a = ap.parse_args()
-names = ["load", "agent_count", "minimap", "obs", "policy+mean", "set_action", "step", "reward", "clear_dead",
+names = ["load", "install", "minimap", "obs", "policy+mean", "set_action", "step", "reward", "clear_dead",
          "episode_reset", "write_back"]
 eng = BattleBatch(64, a.envs, stream=torch.cuda.current_stream())
 left, right = bd.block_positions(64, 128)
 eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1)
+print("rollout grid %d workgroups, %d B dynamic LDS each" % eng.rollout_info())
 buf = torch.zeros(a.envs * 16, dtype=torch.int64, device="cuda")
 assert eng._dll.mfx_battle_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
 eng.rollout_step(400)
 torch.cuda.synchronize()
 acc = []
+conc = []
+inst = []
+sub = []
 for t in range(a.steps):
     eng.rollout_step(1)
     torch.cuda.synchronize()
     st = buf.view(a.envs, 16).cpu().numpy().astype(np.int64)
     acc.append(np.diff(st[:, :11], axis=1))
+    sub.append(np.stack([st[:, 13] - st[:, 0], st[:, 1] - st[:, 13], 10 * (st[:, 11] - st[:, 14])], 1))
+    rt0, rt1 = st[:, 11], st[:, 12]            # s_memrealtime, 100 MHz
+    span = rt1.max() - rt0.min()
+    fr = [0.02, 0.1, 0.3, 0.5, 0.7, 0.9, 0.98]
+    inst.append([((rt0 <= rt0.min() + f * span) & (rt1 >= rt0.min() + f * span)).sum() for f in fr])
+    conc.append(((rt1 - rt0).sum() / span, span / 100.0, (st[:, 10] - st[:, 0]).sum() / (rt1 - rt0).sum() / 100.0))
 d = np.concatenate(acc)
 tot = d.sum(1)
 print("env lifetime (stamp 0 -> 10): median %d cycles, mean %d" % (np.median(tot), tot.mean()))
+c = np.array(conc)
+print("envs in flight (mean over the launch) %.0f; launch span %.0f us; shader clock %.2f GHz"
+      % (c[:, 0].mean(), c[:, 1].mean(), c[:, 2].mean()))
+print("  envs resident at 2/10/30/50/70/90/98%% of the launch:", np.array(inst).mean(0).round().astype(int).tolist())
+sb = np.concatenate(sub)
+print("  install split: LDS stores + barrier mean %d, prefetch issue + barrier mean %d; loop top -> stamp 0 "
+      "mean %d ns" % tuple(sb.mean(0)))
 for i, n in enumerate(names[1:]):
     print("%-14s median %8d  mean %8d  share %5.1f%%" % (n, np.median(d[:, i]), d[:, i].mean(), 100 * d[:, i].mean() / tot.mean()))
