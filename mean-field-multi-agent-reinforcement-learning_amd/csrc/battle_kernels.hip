@@ -212,7 +212,9 @@ struct ObsSmem {                  // LDS carve-up of the observation kernels
     uint16_t* bin;                // [cap] minimap cell of every agent id (this call)
     uint8_t* mask;                // [VH*VW]
     float* type_hp;               // [G]
-    float* hpn;                   // [cap] hp / max hp of every id (wave-streamed path), or null
+    uint32_t* info;               // [cap] wave-streamed path: hp / max hp bits | group << 31, or null
+    uint2* aq;                    // [cap] wave-streamed path: per agent of the group being observed,
+                                  //       view origin (int16 x | int16 y << 16) and minimap bin
 };
 
 // Battle fast path (builtin/config/battle.py): 13x13 view, 7 channels, 2 groups, minimap, 34
@@ -236,8 +238,9 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
             const int b = ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw;
             sm.bin[id] = (uint16_t)b;
             atomicAdd(&sm.hist[j * NV + b], 1);
-            // hp / max hp (Map.cc:208), once per agent instead of once per viewer
-            if (sm.hpn) sm.hpn[id] = v.hp[id] / gp.type[j].hp;
+            // hp / max hp (Map.cc:208), once per agent instead of once per viewer; the group rides
+            // in the sign bit (a visible agent's hp is >= +0)
+            if (sm.info) sm.info[id] = __float_as_uint(v.hp[id] / gp.type[j].hp) | ((uint32_t)j << 31);
         }
     }
     __syncthreads();
@@ -336,12 +339,87 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     __syncthreads();
 }
 
-// ---- Battle fast path, wave-streamed: every wave takes 64 consecutive view cells of the group's
-// output stream (row a, cell c -> stream cell a*169+c), one per lane, computes the cell's 7
-// channels, transposes them through its own 1792-B LDS slice and stores them as 112 float4s
-// (1 KiB contiguous per store instruction).  No workgroup barrier anywhere in the phase.
+// ---- Battle fast path, wave-streamed: every wave takes 128 consecutive view cells of the group's
+// output stream (row a, cell c -> stream cell a*169+c), two per lane, computes each cell's 7
+// channels, transposes them through its own 1792-B LDS slice and stores them as float4s (1 KiB
+// contiguous per store instruction).  No workgroup barrier inside the stream.  Needs the group's
+// agent records (obs_agent_records) and sm.info (obs_minimap).
 constexpr int kWaveCells = 64;
 constexpr int kWaveStageFloats = kWaveCells * BattleShape::NC;   // 448 floats = 1792 B per wave
+
+__device__ __forceinline__ void obs_agent_records(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int g,
+                                                  int n) {
+    const TypeParams& T = gp.type[g];
+    const int32_t* ids = v.grp_ids + g * v.cap;
+    for (int a = TID; a < n; a += blockDim.x) {
+        const int id = ids[a];
+        const uint32_t p = v.xy[id];
+        const int ox = (int)(p & 0xFFFF) + T.view_x1, oy = (int)(p >> 16) + T.view_y1;
+        sm.aq[a] = make_uint2(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16), sm.bin[id]);
+    }
+}
+
+struct CellObs {              // one view cell: kind 0 nothing, 1 wall, 2 own agent, 3 enemy agent
+    float hn, mo, me;
+    int kind;
+};
+
+__device__ __forceinline__ CellObs obs_cell(const EnvView& v, const ObsSmem& sm, const float* mm_own,
+                                            const float* mm_en, int W, int H, int g, int gc, int ncell) {
+    constexpr int NV = BattleShape::VW * BattleShape::VH;
+    CellObs o;
+    o.hn = 0.0f; o.mo = 0.0f; o.me = 0.0f; o.kind = 0;
+    if (gc >= ncell) return o;
+    const int a = gc / NV, c = gc - a * NV;
+    const int vy = c / BattleShape::VW, vx = c - vy * BattleShape::VW;
+    const uint2 q = sm.aq[a];
+    const bool in_view = sm.mask[c] != 0;
+    const bool self = c == (int)q.y;
+    o.mo = mm_own[c]; o.me = mm_en[c];
+    if (self) { o.mo = o.mo + 1.0f; o.me = o.me + 1.0f; }
+    const int mx = (int)(int16_t)(q.x & 0xFFFFu) + vx, my = ((int)q.x >> 16) + vy;
+    if (in_view && mx >= 0 && my >= 0 && mx < W && my < H) {
+        const uint32_t cv = v.cells[my * W + mx];
+        if (cv == kCellWall) {
+            o.kind = 1;
+        } else if (cv != kCellEmpty) {
+            const uint32_t inf = sm.info[cv];
+            o.hn = __uint_as_float(inf & 0x7FFFFFFFu);
+            o.kind = (int)(inf >> 31) == g ? 2 : 3;
+        }
+    }
+    return o;
+}
+
+__device__ __forceinline__ void obs_stage_cell(float* st, int lane, const CellObs& o) {
+    float* d = st + lane * BattleShape::NC;
+    d[0] = o.kind == 1 ? 1.0f : 0.0f;
+    d[1] = o.kind == 2 ? 1.0f : 0.0f;
+    d[2] = o.kind == 2 ? o.hn : 0.0f;
+    d[3] = o.mo;
+    d[4] = o.kind == 3 ? 1.0f : 0.0f;
+    d[5] = o.kind == 3 ? o.hn : 0.0f;
+    d[6] = o.me;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// copy one staged 64-cell block (cells valid cells) to dst, 16-B aligned when cells == 64
+__device__ __forceinline__ void obs_flush(float* __restrict__ dst, const float* st, int lane, int cells) {
+    constexpr int NC = BattleShape::NC;
+    if (cells == kWaveCells) {
+        const float4* s4 = reinterpret_cast<const float4*>(st);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        d4[lane] = s4[lane];
+        if (lane < kWaveStageFloats / 4 - 64) d4[64 + lane] = s4[64 + lane];
+    } else {
+        for (int i = lane; i < cells * NC; i += 64) dst[i] = st[i];
+    }
+}
 
 __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int g,
                                                   int n, float* __restrict__ out_view, float* __restrict__ out_feat,
@@ -350,56 +428,24 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
     const int lane = TID & 63, wid = TID >> 6, nw = blockDim.x >> 6;
     const int W = gp.W, H = gp.H;
     const TypeParams& T = gp.type[g];
-    const int vx1 = T.view_x1, vy1 = T.view_y1;
     const int32_t* ids = v.grp_ids + g * v.cap;
     const float* mm_own = sm.mm + g * NV;
     const float* mm_en = sm.mm + (g ^ 1) * NV;
     float* st = wave_stage + wid * kWaveStageFloats;
     const int ncell = n * NV;
-    for (int base = wid * kWaveCells; base < ncell; base += nw * kWaveCells) {
-        const int gc = base + lane;
-        float x[NC];
-#pragma unroll
-        for (int k = 0; k < NC; ++k) x[k] = 0.0f;
-        if (gc < ncell) {
-            const int a = gc / NV, c = gc - a * NV;
-            const int vy = c / BattleShape::VW, vx = c - vy * BattleShape::VW;
-            const int id = ids[a];
-            const uint32_t pos = v.xy[id];
-            const int mx = (int)(pos & 0xFFFF) + vx1 + vx, my = (int)(pos >> 16) + vy1 + vy;
-            if (sm.mask[c] && mx >= 0 && my >= 0 && mx < W && my < H) {
-                const uint32_t cv = v.cells[my * W + mx];
-                if (cv == kCellWall) {
-                    x[0] = 1.0f;
-                } else if (cv != kCellEmpty) {
-                    const float hn = sm.hpn[cv];
-                    if ((int)meta_group(v.meta[cv]) == g) { x[1] = 1.0f; x[2] = hn; }
-                    else { x[4] = 1.0f; x[5] = hn; }
-                }
-            }
-            const bool self = c == (int)sm.bin[id];
-            const float mo = mm_own[c], me = mm_en[c];
-            x[3] = self ? mo + 1.0f : mo;
-            x[6] = self ? me + 1.0f : me;
+    for (int base = wid * 2 * kWaveCells; base < ncell; base += nw * 2 * kWaveCells) {
+        const CellObs o0 = obs_cell(v, sm, mm_own, mm_en, W, H, g, base + lane, ncell);
+        const CellObs o1 = obs_cell(v, sm, mm_own, mm_en, W, H, g, base + kWaveCells + lane, ncell);
+        obs_stage_cell(st, lane, o0);
+        wave_sync_lds();
+        obs_flush(out_view + (size_t)base * NC, st, lane, min(kWaveCells, ncell - base));
+        wave_sync_lds();
+        if (base + kWaveCells < ncell) {
+            obs_stage_cell(st, lane, o1);
+            wave_sync_lds();
+            obs_flush(out_view + (size_t)(base + kWaveCells) * NC, st, lane, min(kWaveCells, ncell - base - kWaveCells));
+            wave_sync_lds();
         }
-#pragma unroll
-        for (int k = 0; k < NC; ++k) st[lane * NC + k] = x[k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int cells = min(kWaveCells, ncell - base);
-        float* dst = out_view + (size_t)base * NC;        // base % 64 == 0 -> 16-B aligned
-        if (cells == kWaveCells) {
-            const float4* s4 = reinterpret_cast<const float4*>(st);
-            float4* d4 = reinterpret_cast<float4*>(dst);
-            d4[lane] = s4[lane];
-            if (lane < kWaveStageFloats / 4 - 64) d4[64 + lane] = s4[64 + lane];
-        } else {
-            for (int i = lane; i < cells * NC; i += 64) dst[i] = st[i];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // features (GridWorld.cc:411-421): consecutive lanes write consecutive floats
     const int emb = gp.emb, na = T.n_action;
@@ -436,7 +482,7 @@ __host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t NV = (size_t)gp.type[g].view_w * gp.type[g].view_h;
     return r16(stage_floats * 4) + r16((size_t)gp.n_groups * NV * 4) + r16((size_t)cap * 2) + 16 + r16(NV) +
-           r16((size_t)cap * 4);
+           r16((size_t)cap * 4) + r16((size_t)cap * 8);
 }
 
 __device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, int cap, size_t stage_floats,
@@ -451,7 +497,8 @@ __device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, i
     sm.bin = reinterpret_cast<uint16_t*>(smem + off); off += r16((size_t)cap * 2);
     sm.type_hp = reinterpret_cast<float*>(smem + off); off += 16;
     sm.mask = reinterpret_cast<uint8_t*>(smem + off); off += r16(NV);
-    sm.hpn = reinterpret_cast<float*>(smem + off);   off += r16((size_t)cap * 4);
+    sm.info = reinterpret_cast<uint32_t*>(smem + off); off += r16((size_t)cap * 4);
+    sm.aq = reinterpret_cast<uint2*>(smem + off);     off += r16((size_t)cap * 8);
     return sm;
 }
 
@@ -484,7 +531,7 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     if (a_end > rowcap) { if (TID == 0) set_err(s, 4); return; }
     size_t off = 0;
     ObsSmem sm = carve_obs(smem, gp, g, s.cap, obs_stage_floats(gp, g, kB, blockDim.x), off);
-    if (!kB) sm.hpn = nullptr;
+    if (!kB) sm.info = nullptr;
     if (cells_in_lds) {
         uint16_t* lc = reinterpret_cast<uint16_t*>(smem + off);
         const int n2 = s.cells_n;
@@ -501,6 +548,8 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     if (kB) {
         EnvView vc = v;                      // rows [a_begin, a_end): shift the group list and outputs
         vc.grp_ids = v.grp_ids + a_begin;
+        obs_agent_records(gp, vc, sm, g, a_end - a_begin);
+        __syncthreads();
         obs_stream_battle(gp, vc, sm, g, a_end - a_begin, ov + (size_t)a_begin * VF, of + (size_t)a_begin * F, sm.stage);
     } else {
         for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows<kB>(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
@@ -1273,7 +1322,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
     char* uni = smem + soff;                 // scratch shared by the observation and the step phases
     size_t soff2 = soff;
     ObsSmem osm = carve_obs(smem, gp, 0, cap, obs_stage_floats(gp, 0, kB, blockDim.x), soff2);
-    if (!kB) osm.hpn = nullptr;
+    if (!kB) osm.info = nullptr;
     const RolloutUnion u = rollout_union(gp, cap, acap, blockDim.x);
     int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
     int* ahist = reinterpret_cast<int*>(uni + u.ahist);
@@ -1313,7 +1362,10 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
             float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
             const int n = min(v.grp_n[g], ra.rowcap);
             if (kB) {
+                obs_agent_records(gp, v, osm, g, n);
+                __syncthreads();
                 obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
+                __syncthreads();               // the records are rebuilt for the next group
             } else {
                 obs_prologue(gp, osm, g);
                 __syncthreads();
