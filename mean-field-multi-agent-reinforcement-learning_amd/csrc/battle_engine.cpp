@@ -300,6 +300,8 @@ public:
                 RP.val[k] = R.val[k];
             }
         }
+        p.par_step = 1;
+        for (int g = 0; g < p.n_groups; g++) p.par_step &= p.type[g].kill_supply == 0.0f;
         gp = p;
         return 0;
     }

@@ -364,30 +364,29 @@ struct CellObs {              // one view cell: kind 0 nothing, 1 wall, 2 own ag
     int kind;
 };
 
+// Branch-free: every LDS read is issued from a safe index and the results are selected, so a wave
+// never splits its exec mask (the branchy form spent ~40 % of its instructions on mask bookkeeping).
 __device__ __forceinline__ CellObs obs_cell(const EnvView& v, const ObsSmem& sm, const float* mm_own,
                                             const float* mm_en, int W, int H, int g, int gc, int ncell) {
     constexpr int NV = BattleShape::VW * BattleShape::VH;
-    CellObs o;
-    o.hn = 0.0f; o.mo = 0.0f; o.me = 0.0f; o.kind = 0;
-    if (gc >= ncell) return o;
-    const int a = gc / NV, c = gc - a * NV;
+    const bool valid = gc < ncell;
+    const int gs = valid ? gc : 0;
+    const int a = gs / NV, c = gs - a * NV;
     const int vy = c / BattleShape::VW, vx = c - vy * BattleShape::VW;
     const uint2 q = sm.aq[a];
-    const bool in_view = sm.mask[c] != 0;
+    const uint32_t mk = sm.mask[c];
+    const float mo = mm_own[c], me = mm_en[c];
     const bool self = c == (int)q.y;
-    o.mo = mm_own[c]; o.me = mm_en[c];
-    if (self) { o.mo = o.mo + 1.0f; o.me = o.me + 1.0f; }
     const int mx = (int)(int16_t)(q.x & 0xFFFFu) + vx, my = ((int)q.x >> 16) + vy;
-    if (in_view && mx >= 0 && my >= 0 && mx < W && my < H) {
-        const uint32_t cv = v.cells[my * W + mx];
-        if (cv == kCellWall) {
-            o.kind = 1;
-        } else if (cv != kCellEmpty) {
-            const uint32_t inf = sm.info[cv];
-            o.hn = __uint_as_float(inf & 0x7FFFFFFFu);
-            o.kind = (int)(inf >> 31) == g ? 2 : 3;
-        }
-    }
+    const bool ok = valid && mk != 0 && (unsigned)mx < (unsigned)W && (unsigned)my < (unsigned)H;
+    const uint32_t cv = v.cells[ok ? my * W + mx : 0];
+    const bool agent = ok && cv < kCellWall;
+    const uint32_t inf = sm.info[agent ? cv : 0];
+    CellObs o;
+    o.mo = valid ? (self ? mo + 1.0f : mo) : 0.0f;
+    o.me = valid ? (self ? me + 1.0f : me) : 0.0f;
+    o.hn = agent ? __uint_as_float(inf & 0x7FFFFFFFu) : 0.0f;
+    o.kind = (ok && cv == kCellWall) ? 1 : (agent ? ((int)(inf >> 31) == g ? 2 : 3) : 0);
     return o;
 }
 
@@ -402,10 +401,12 @@ __device__ __forceinline__ void obs_stage_cell(float* st, int lane, const CellOb
     d[6] = o.me;
 }
 
+// LDS hand-off between the lanes of ONE wave.  An asm memory clobber, not wavefront fences: from a
+// single lane's view a write to x[lane] and a read of x[lane + k] never alias, so without a real
+// compiler barrier the read may be hoisted above the other lanes' writes.
 __device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // copy one staged 64-cell block (cells valid cells) to dst, 16-B aligned when cells == 64
@@ -704,16 +705,277 @@ __device__ __forceinline__ void do_move_one(const GameParams& gp, const StepSmem
     }
 }
 
+// ==================================================================================
+//  parallel exact resolution of the order-dependent part of the step (gp.par_step)
+// ==================================================================================
+// The reference resolves the shuffled attacks and then the moves one by one
+// (GridWorld.cc:507-558, 631-672).  The same results come out of a few data-parallel passes:
+//  * shuffle: x_k = 16807^(k+1) x0 mod (2^31-1) (minstd jump-ahead), so every j_k = x_k % (k+1)
+//    is independent; the forward Fisher-Yates then moves element i to j_i and on to k whenever a
+//    later j_k hits its current position.
+//  * attacks: with kill_supply == 0 a kill changes nothing but the victim, so the outcome is fixed
+//    by the position at which each agent dies.  Iterate: assume the current death positions, let
+//    every attack replay the sequential hp updates of its target up to itself (hits of attackers
+//    still alive at their turn), and record where each target now dies.  Iteration t fixes the
+//    t-th kill in shuffle order, so the loop ends after (#kills + 1) passes.
+//  * moves: a mover may be resolved once it is the earliest unresolved mover that touches its
+//    source or its target cell -- every earlier event on both cells is then applied, and no later
+//    one is.  Rounds of "claim both cells (atomicMin), resolve the owners" reach the fixed
+//    sequential order; a hashed claim table only adds false conflicts (extra rounds).
+constexpr int kOwnerSlots = 512;
+constexpr int16_t kNoDeath = 0x7FFF;
+
+struct ParScratch {
+    uint32_t* ord;       // [acap] attack entries in shuffled order
+    uint16_t* jv;        // [acap] Fisher-Yates j_k
+    uint16_t* att;       // [acap] attacker id by position
+    int16_t* tgt;        // [acap] target id at phase start; -1 blank; -2 attacker already dead
+    int16_t* eff;        // [acap] target if this position is a hit under the current deaths, else -1
+    float* dmg;          // [acap] attacker damage by position
+    int16_t* death;      // [cap] position of the attack that kills id, or kNoDeath
+    int16_t* death_new;  // [cap]
+    uint32_t* owner;     // [kOwnerSlots] move rounds (aliases the attack arrays)
+    int* flag;           // [1]
+};
+
+__host__ __device__ inline size_t par_scratch_bytes(int acap, int cap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t atk = r16((size_t)acap * 4) + 3 * r16((size_t)acap * 2) + r16((size_t)acap * 2) +
+                       r16((size_t)acap * 4) + 2 * r16((size_t)cap * 2);
+    const size_t mov = r16((size_t)kOwnerSlots * 4);
+    return (atk > mov ? atk : mov) + 16;
+}
+
+__device__ __forceinline__ ParScratch carve_par(char* base, int acap, int cap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    ParScratch p;
+    size_t o = 0;
+    p.ord = reinterpret_cast<uint32_t*>(base + o);  o += r16((size_t)acap * 4);
+    p.jv = reinterpret_cast<uint16_t*>(base + o);   o += r16((size_t)acap * 2);
+    p.att = reinterpret_cast<uint16_t*>(base + o);  o += r16((size_t)acap * 2);
+    p.tgt = reinterpret_cast<int16_t*>(base + o);   o += r16((size_t)acap * 2);
+    p.eff = reinterpret_cast<int16_t*>(base + o);   o += r16((size_t)acap * 2);
+    p.dmg = reinterpret_cast<float*>(base + o);     o += r16((size_t)acap * 4);
+    p.death = reinterpret_cast<int16_t*>(base + o); o += r16((size_t)cap * 2);
+    p.death_new = reinterpret_cast<int16_t*>(base + o); o += r16((size_t)cap * 2);
+    p.owner = reinterpret_cast<uint32_t*>(base);    // move rounds run after the attacks
+    const size_t mov = r16((size_t)kOwnerSlots * 4);
+    p.flag = reinterpret_cast<int*>(base + (o > mov ? o : mov));
+    return p;
+}
+
+__device__ __forceinline__ uint32_t mulmod_m31(uint32_t a, uint32_t b) {
+    uint64_t p = (uint64_t)a * b;
+    p = (p & 0x7FFFFFFFull) + (p >> 31);
+    p = (p & 0x7FFFFFFFull) + (p >> 31);
+    if (p >= 0x7FFFFFFFull) p -= 0x7FFFFFFFull;
+    return (uint32_t)p;
+}
+
+__device__ __forceinline__ uint32_t minstd_jump(uint32_t x0, uint32_t k) {   // k draws ahead of x0
+    uint32_t r = x0, b = 16807u;
+    while (k) {
+        if (k & 1u) r = mulmod_m31(r, b);
+        b = mulmod_m31(b, b);
+        k >>= 1;
+    }
+    return r;
+}
+
+// kWave: the pass runs on wave 0 alone (n <= 64) and every barrier is a wave-level LDS sync;
+// otherwise the whole workgroup takes part (n <= blockDim.x).
+template <bool kWave>
+__device__ __forceinline__ void psync() {
+    if (kWave) wave_sync_lds();
+    else __syncthreads();
+}
+
+// Shuffle + attack resolution for n_atk <= lanes.  Leaves the attack effects applied to v.
+template <bool kWave>
+__device__ void attack_parallel(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* atk,
+                                int n, uint32_t& rng, const ParScratch& ps, int nid) {
+    const int t = TID, W = gp.W, H = gp.H;
+    // ---- shuffle
+    uint32_t ent = 0;
+    if (t < n) {
+        ent = atk[t];
+        const uint32_t x = minstd_jump(rng, (uint32_t)t + 1u);
+        ps.jv[t] = (uint16_t)(x % (uint32_t)(t + 1));
+        if (t == n - 1) ps.flag[0] = (int)x;
+    }
+    for (int id = t; id < nid; id += (kWave ? 64 : (int)blockDim.x)) ps.death[id] = kNoDeath;
+    psync<kWave>();
+    if (n > 0) rng = (uint32_t)ps.flag[0];
+    if (t < n) {
+        int p = ps.jv[t];
+        for (int k = t + 1; k < n; ++k) if (ps.jv[k] == p) p = k;
+        ps.ord[p] = ent;
+    }
+    psync<kWave>();
+    // ---- per position: attacker, damage, target at phase start
+    int A = -1, T = -2;
+    if (t < n) {
+        const uint32_t e2 = ps.ord[t];
+        A = (int)(e2 >> 8);
+        const int ai = (int)(e2 & 0xFF);
+        const uint32_t m = v.meta[A];
+        if (!meta_dead(m)) {
+            const int g = meta_group(m);
+            const SerialType& S = sm.tt[g];
+            const uint32_t pos = v.xy[A];
+            const int ox = (int)(pos & 0xFFFF) + S.att_x_off + S.att_dx[ai];
+            const int oy = (int)(pos >> 16) + S.att_y_off + S.att_dy[ai];
+            uint32_t cv = kCellEmpty;
+            if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
+            T = -1;
+            if (cv < kCellWall && (S.attack_in_group || (int)meta_group(v.meta[cv]) != g)) T = (int)cv;
+            ps.dmg[t] = S.damage;
+        }
+        ps.att[t] = (uint16_t)A;
+        ps.tgt[t] = (int16_t)T;
+    }
+    psync<kWave>();
+    // ---- fixed point on the death positions
+    for (int it = 0; it <= n + 1; ++it) {
+        if (t < n) ps.eff[t] = (T >= 0 && ps.death[A] > t) ? (int16_t)T : (int16_t)-1;
+        for (int id = t; id < nid; id += (kWave ? 64 : (int)blockDim.x)) ps.death_new[id] = kNoDeath;
+        if (t == 0) ps.flag[0] = 0;
+        psync<kWave>();
+        if (t < n && ps.eff[t] >= 0) {
+            float h = v.hp[T];
+            for (int q = 0; q <= t; ++q) {
+                if (ps.eff[q] != T) continue;
+                h = h - ps.dmg[q];                               // Agent::be_attack
+                if (h < 0.0f) {
+                    if (q == t) ps.death_new[T] = (int16_t)t;
+                    break;
+                }
+            }
+        }
+        psync<kWave>();
+        for (int id = t; id < nid; id += (kWave ? 64 : (int)blockDim.x))
+            if (ps.death_new[id] != ps.death[id]) { ps.death[id] = ps.death_new[id]; ps.flag[0] = 1; }
+        psync<kWave>();
+        if (!ps.flag[0]) break;
+        psync<kWave>();
+    }
+    // ---- apply: attackers (each agent attacks at most once per step), then hp, then deaths.
+    // eff = the hits; jv / ord (free after the shuffle) carry "last hit on its target" / its hp.
+    if (t < n) ps.eff[t] = (T >= 0 && ps.death[A] > t && ps.death[T] >= t) ? (int16_t)T : (int16_t)-1;
+    psync<kWave>();
+    bool last = false;
+    if (t < n && T != -2 && ps.death[A] > t) {
+        const uint32_t m = v.meta[A];
+        const int g = meta_group(m);
+        const SerialType& S = sm.tt[g];
+        if (ps.eff[t] < 0) {
+            v.next_r[A] += S.attack_penalty;                     // blank area (or a dead target)
+        } else {
+            const bool kill = ps.death[T] == t;
+            v.meta[A] = (uint8_t)meta_make(0, kill ? kOpKill : kOpAttack, g);
+            v.op_obj[A] = T;
+            const float reward = kill ? sm.tt[meta_group(v.meta[T])].kill_reward : 0.0f;
+            v.next_r[A] += reward + S.attack_penalty;
+            // the last hit on T sets its hp: replay the hits on T up to this one
+            last = true;
+            for (int q = t + 1; q < n; ++q) if (ps.eff[q] == T) { last = false; break; }
+            if (last) {
+                float h = v.hp[T];
+                for (int q = 0; q <= t; ++q) if (ps.eff[q] == T) h = h - ps.dmg[q];
+                ps.ord[t] = __float_as_uint(h);
+            }
+        }
+    }
+    psync<kWave>();
+    if (last) v.hp[T] = __uint_as_float(ps.ord[t]);
+    for (int id = t; id < nid; id += (kWave ? 64 : (int)blockDim.x)) {
+        if (ps.death[id] == kNoDeath) continue;
+        const uint32_t om = v.meta[id];
+        const int og = meta_group(om);
+        v.meta[id] = (uint8_t)meta_make(1, meta_op(om), og);
+        v.next_r[id] = sm.tt[og].dead_penalty;
+        const uint32_t pos = v.xy[id];
+        v.cells[(pos >> 16) * W + (pos & 0xFFFF)] = kCellEmpty;   // remove_agent
+        atomicAdd(&v.grp_dead[og], 1);
+    }
+    psync<kWave>();
+}
+
+// Move resolution for n_mov <= lanes in `order` (buffer order, or band order on large maps).
+template <bool kWave>
+__device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n,
+                              const ParScratch& ps) {
+    const int t = TID, W = gp.W, H = gp.H;
+    int id = -1, src = 0, dst = 0, nx = 0, ny = 0;
+    bool pending = false;
+    if (t < n) {
+        const uint32_t ent = order[t];
+        id = (int)(ent >> 16);
+        const int mi = (int)((ent >> 8) & 0xFF);
+        const uint32_t m = v.meta[id];
+        if (!meta_dead(m)) {
+            const SerialType& S = sm.tt[meta_group(m)];
+            const uint32_t p = v.xy[id];
+            const int x = p & 0xFFFF, y = p >> 16;
+            nx = x + S.move_dx[mi]; ny = y + S.move_dy[mi];
+            // out of board: no-op; a move onto itself succeeds without changing anything
+            pending = !(nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) && !(nx == x && ny == y);
+            src = y * W + x; dst = ny * W + nx;
+        }
+    }
+    const uint32_t hs = (uint32_t)src % kOwnerSlots, hd = (uint32_t)dst % kOwnerSlots;
+    for (int round = 0; round <= n; ++round) {
+        for (int k = t; k < kOwnerSlots; k += (kWave ? 64 : (int)blockDim.x)) ps.owner[k] = 0xFFFFFFFFu;
+        if (t == 0) ps.flag[0] = 0;
+        psync<kWave>();
+        if (pending) { atomicMin(&ps.owner[hs], (uint32_t)t); atomicMin(&ps.owner[hd], (uint32_t)t); }
+        psync<kWave>();
+        if (pending) {
+            if (ps.owner[hs] == (uint32_t)t && ps.owner[hd] == (uint32_t)t) {
+                const uint32_t cv = v.cells[dst];
+                if (cv == kCellEmpty) {
+                    v.cells[src] = kCellEmpty;
+                    v.cells[dst] = (uint16_t)id;
+                    v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
+                } else if (cv != kCellWall) {
+                    v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(v.meta[id]));
+                    v.op_obj[id] = (int)cv;
+                }
+                pending = false;
+            } else {
+                ps.flag[0] = 1;
+            }
+        }
+        psync<kWave>();
+        if (!ps.flag[0]) break;
+        psync<kWave>();
+    }
+}
+
 // Everything of GridWorld::step for one env, executed by the whole workgroup.
 // atk/mov/sorted: pending buffers (any address space); sorted has room for n_mov entries.
 // sm.tt must hold the serial type table (load_serial_types + barrier).
+// ps: LDS scratch for the parallel resolution (nullptr: one-lane loops only); nid = id_counter.
 __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
                               uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
-                              int& done_out) {
+                              int& done_out, const ParScratch* ps, int nid) {
     const int G = gp.n_groups;
+#ifndef MFX_PAR_MASK
+#define MFX_PAR_MASK 3
+#endif
+    const bool par0 = ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x;
+    bool par = par0 && (MFX_PAR_MASK & 1);
     __syncthreads();
-    // ---- shuffle + attack: one lane (GridWorld.cc:507-558)
-    if (TID == 0) {
+    // ---- shuffle + attack (GridWorld.cc:507-558)
+#ifndef MFX_WAVE_STEP_MAX
+#define MFX_WAVE_STEP_MAX 64
+#endif
+    if (par && n_atk <= MFX_WAVE_STEP_MAX) {
+        if (TID < 64) attack_parallel<true>(gp, sm, v, atk, n_atk, rng, *ps, nid);
+        __syncthreads();
+    } else if (par) {
+        attack_parallel<false>(gp, sm, v, atk, n_atk, rng, *ps, nid);
+    } else if (TID == 0) {
         uint32_t x = rng;
         for (int i = 0; i < n_atk; ++i) {
             x = minstd_next(x);
@@ -768,9 +1030,17 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         __syncthreads();
         order = sorted;
     }
-    if (TID == 0)
-        for (int i = 0; i < n_mov; ++i) do_move_one(gp, sm, v, order[i]);
-    __syncthreads();
+    par = par0 && (MFX_PAR_MASK & 2);
+    if (par && n_mov <= MFX_WAVE_STEP_MAX) {
+        if (TID < 64) move_parallel<true>(gp, sm, v, order, n_mov, *ps);
+        __syncthreads();
+    } else if (par) {
+        move_parallel<false>(gp, sm, v, order, n_mov, *ps);
+    } else {
+        if (TID == 0)
+            for (int i = 0; i < n_mov; ++i) do_move_one(gp, sm, v, order[i]);
+        __syncthreads();
+    }
     // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
     for (int r = 0; r < gp.n_rules; ++r) {
         const RuleParams& R = gp.rules[r];
@@ -852,7 +1122,7 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     uint32_t rng = s.rng[e];
     int done = 0;
     load_serial_types(gp, sm);
-    step_env_core(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done);
+    step_env_core(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, nullptr, nid);
     if (lds) {
         for (int i = TID; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
         for (int i = TID; i < nid; i += blockDim.x) {
@@ -985,7 +1255,7 @@ __device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-o
 // LDS plan of k_rollout: the env (cells, per-id arrays, group lists) stays resident for the whole
 // launch; one scratch region is shared by the observation phase (minimap, bins, hp/max, staging) and
 // the policy/step phase (actions, histogram, attack/move buffers; the reduction reuses the actions).
-struct RolloutUnion { size_t act, ahist, atk, mov, sorted, red, total; };
+struct RolloutUnion { size_t act, ahist, atk, mov, sorted, red, par, total; };
 
 __host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int cap, int acap, int threads) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -997,6 +1267,7 @@ __host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int 
     u.atk = o;    o += r16((size_t)acap * 4);
     u.mov = o;    o += r16((size_t)acap * 4);
     u.sorted = o; o += gp.large_map ? r16((size_t)acap * 4) : 0;
+    u.par = o;    o += gp.par_step ? r16(par_scratch_bytes(acap, cap)) : 0;
     u.total = o;
     return u;
 }
@@ -1404,7 +1675,8 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
         MFX_STAMP(5);
         uint32_t rng = sc.rng;
         int done = 0;
-        step_env_core(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done);
+        const ParScratch ps = carve_par(uni + u.par, acap, cap);
+        step_env_core(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, &ps, sc.id_counter);
         MFX_STAMP(6);
         // ---------------- get_reward, episode return, kills
         float kills = 0.0f;

@@ -66,6 +66,8 @@ struct GameParams {
     int W, H, n_groups, minimap, emb, n_ch;
     int large_map, n_sep, band_w;
     int n_rules;
+    int par_step;                   // 1: attack / move resolution may run in parallel (every
+                                    //    kill_supply == 0, so a kill never changes the killer's hp)
     int feat_size[kMaxGroups];
     TypeParams type[kMaxGroups];    // per group (Group::type)
     RuleParams rules[kMaxRules];

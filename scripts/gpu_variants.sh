@@ -1,0 +1,6 @@
+# bench several library variants back to back: scripts/gpu_variants.sh name1 name2 ...
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+B=$GRAFT_REPO_ROOT/mean-field-multi-agent-reinforcement-learning_amd/build
+for n in "$@"; do
+  MAGENT_LIB=$B/libmagent_$n.so timeout -k 10 300 python bench.py --steps 50 --warmup 5 --envs 16384 --no-cpu-baseline > gpurun_out/var_$n.json 2> gpurun_out/var_$n.err || exit 1
+done
