@@ -436,12 +436,12 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
     const int ncell = n * NV;
     for (int base = wid * 2 * kWaveCells; base < ncell; base += nw * 2 * kWaveCells) {
         const CellObs o0 = obs_cell(v, sm, mm_own, mm_en, W, H, g, base + lane, ncell);
-        const CellObs o1 = obs_cell(v, sm, mm_own, mm_en, W, H, g, base + kWaveCells + lane, ncell);
         obs_stage_cell(st, lane, o0);
         wave_sync_lds();
         obs_flush(out_view + (size_t)base * NC, st, lane, min(kWaveCells, ncell - base));
         wave_sync_lds();
         if (base + kWaveCells < ncell) {
+            const CellObs o1 = obs_cell(v, sm, mm_own, mm_en, W, H, g, base + kWaveCells + lane, ncell);
             obs_stage_cell(st, lane, o1);
             wave_sync_lds();
             obs_flush(out_view + (size_t)(base + kWaveCells) * NC, st, lane, min(kWaveCells, ncell - base - kWaveCells));
