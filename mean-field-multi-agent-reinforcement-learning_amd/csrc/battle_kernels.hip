@@ -31,8 +31,14 @@ __device__ unsigned long long* g_stamps;
             if ((i) == 10) g_stamps[stamp_row * 16 + 12] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                                   \
     } while (0)
+#define MFX_TSTAMP(kW, i)                                                                   \
+    do {                                                                                    \
+        psync<kW>();                                                                        \
+        if (TID == 0 && g_stamps) g_stamps[stamp_row * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define MFX_STAMP(i) do {} while (0)
+#define MFX_TSTAMP(kW, i) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- utils
@@ -409,6 +415,31 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// A "team" runs the per-agent phases of an env: the whole workgroup, or wave 0 alone (kWave) when
+// every per-agent count fits in 64 lanes -- then each barrier is a wave-level LDS sync and scans
+// and sums are ballots and lane shuffles.
+template <bool kWave>
+__device__ __forceinline__ void psync() {
+    if (kWave) wave_sync_lds();
+    else __syncthreads();
+}
+
+template <bool kWave>
+__device__ __forceinline__ int team_lanes() { return kWave ? 64 : (int)blockDim.x; }
+
+template <bool kWave>
+__device__ __forceinline__ int team_scan(int flag, int* wave_tot, int& total) {
+    if (!kWave) return block_scan_flag(flag, wave_tot, total);
+    const unsigned long long m = __ballot(flag);
+    total = __popcll(m);
+    return __popcll(m & ((1ull << (TID & 63)) - 1ull));
+}
+
+__device__ __forceinline__ float wave_sum(float x) {         // fixed butterfly order
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
 // copy one staged 64-cell block (cells valid cells) to dst, 16-B aligned when cells == 64
 __device__ __forceinline__ void obs_flush(float* __restrict__ dst, const float* st, int lane, int cells) {
     constexpr int NC = BattleShape::NC;
@@ -560,14 +591,15 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
 // ==================================================================================
 //  set_action (GridWorld.cc:430-496): classify in call order and append to the buffers.
 // ==================================================================================
+template <bool kW>
 __device__ __forceinline__ void set_action_group(const GameParams& gp, const State& s, EnvView& v, int g,
                                                  const int* __restrict__ acts, uint32_t* atk, int& n_atk,
                                                  uint32_t* mov, int& n_mov, int* wave_tot, int acap) {
     const TypeParams& T = gp.type[g];
     const int n = v.grp_n[g];
     int base_a = n_atk, base_m = n_mov;
-    __syncthreads();
-    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+    psync<kW>();
+    for (int i0 = 0; i0 < n; i0 += team_lanes<kW>()) {
         const int i = i0 + TID;
         int a = 0, id = 0, is_move = 0, is_atk = 0;
         uint32_t bucket = kBucketBoundary;
@@ -584,17 +616,17 @@ __device__ __forceinline__ void set_action_group(const GameParams& gp, const Sta
             }
         }
         int tot_m, tot_a;
-        const int rm = block_scan_flag(is_move, wave_tot, tot_m);
-        const int ra = block_scan_flag(is_atk, wave_tot, tot_a);
+        const int rm = team_scan<kW>(is_move, wave_tot, tot_m);
+        const int ra = team_scan<kW>(is_atk, wave_tot, tot_a);
         if (is_move && base_m + rm < acap) mov[base_m + rm] = ((uint32_t)id << 16) | ((uint32_t)a << 8) | bucket;
         if (is_atk && base_a + ra < acap) atk[base_a + ra] = ((uint32_t)id << 8) | (uint32_t)(a - T.attack_base);
         base_m += tot_m;
         base_a += tot_a;
     }
     if (base_m > acap || base_a > acap) { if (TID == 0) set_err(s, 6); }
-    __syncthreads();
+    psync<kW>();
     if (TID == 0) { n_atk = min(base_a, acap); n_mov = min(base_m, acap); }
-    __syncthreads();
+    psync<kW>();
 }
 
 __global__ void __launch_bounds__(256) k_set_action(const GameParams* __restrict__ gp, State s, int g,
@@ -603,7 +635,7 @@ __global__ void __launch_bounds__(256) k_set_action(const GameParams* __restrict
     const int e = blockIdx.x;
     EnvView v = global_view(s, e, gp->n_groups);
     if (v.grp_n[g] > rowcap) { if (TID == 0) set_err(s, 4); return; }
-    set_action_group(*gp, s, v, g, actions + (size_t)e * rowcap, s.atk + (size_t)e * s.acap, s.n_atk[e],
+    set_action_group<false>(*gp, s, v, g, actions + (size_t)e * rowcap, s.atk + (size_t)e * s.acap, s.n_atk[e],
                      s.mov + (size_t)e * s.acap, s.n_mov[e], wave_tot, s.acap);
 }
 
@@ -782,13 +814,6 @@ __device__ __forceinline__ uint32_t minstd_jump(uint32_t x0, uint32_t k) {   // 
     return r;
 }
 
-// kWave: the pass runs on wave 0 alone (n <= 64) and every barrier is a wave-level LDS sync;
-// otherwise the whole workgroup takes part (n <= blockDim.x).
-template <bool kWave>
-__device__ __forceinline__ void psync() {
-    if (kWave) wave_sync_lds();
-    else __syncthreads();
-}
 
 // Shuffle + attack resolution for n_atk <= lanes.  Leaves the attack effects applied to v.
 template <bool kWave>
@@ -956,25 +981,28 @@ __device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView&
 // atk/mov/sorted: pending buffers (any address space); sorted has room for n_mov entries.
 // sm.tt must hold the serial type table (load_serial_types + barrier).
 // ps: LDS scratch for the parallel resolution (nullptr: one-lane loops only); nid = id_counter.
+template <bool kW>
 __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
                               uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
-                              int& done_out, const ParScratch* ps, int nid) {
+                              int& done_out, const bool have_ps, const ParScratch ps, int nid) {
     const int G = gp.n_groups;
 #ifndef MFX_PAR_MASK
 #define MFX_PAR_MASK 3
 #endif
-    const bool par0 = ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x;
+    const bool par0 = have_ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x;
     bool par = par0 && (MFX_PAR_MASK & 1);
-    __syncthreads();
+    psync<kW>();
     // ---- shuffle + attack (GridWorld.cc:507-558)
 #ifndef MFX_WAVE_STEP_MAX
 #define MFX_WAVE_STEP_MAX 64
 #endif
-    if (par && n_atk <= MFX_WAVE_STEP_MAX) {
-        if (TID < 64) attack_parallel<true>(gp, sm, v, atk, n_atk, rng, *ps, nid);
+    if (kW && par) {
+        attack_parallel<true>(gp, sm, v, atk, n_atk, rng, ps, nid);
+    } else if (par && n_atk <= MFX_WAVE_STEP_MAX) {
+        if (TID < 64) attack_parallel<true>(gp, sm, v, atk, n_atk, rng, ps, nid);
         __syncthreads();
     } else if (par) {
-        attack_parallel<false>(gp, sm, v, atk, n_atk, rng, *ps, nid);
+        attack_parallel<false>(gp, sm, v, atk, n_atk, rng, ps, nid);
     } else if (TID == 0) {
         uint32_t x = rng;
         for (int i = 0; i < n_atk; ++i) {
@@ -985,12 +1013,12 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         rng = x;
         do_attack_serial(gp, sm, v, atk, n_atk);
     }
-    __syncthreads();
+    psync<kW>();
     // ---- starve (GridWorld.cc:570-595): independent per agent
     for (int g = 0; g < G; ++g) {
         const TypeParams& T = gp.type[g];
         const int n = v.grp_n[g];
-        for (int i = TID; i < n; i += blockDim.x) {
+        for (int i = TID; i < n; i += team_lanes<kW>()) {
             const int id = v.grp_ids[g * v.cap + i];
             const uint32_t m = v.meta[id];
             if (meta_dead(m)) continue;
@@ -1010,36 +1038,38 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
             }
         }
     }
-    __syncthreads();
+    psync<kW>();
     // ---- move order: large map = band buffers 0..n_sep-1 then boundary (GridWorld.cc:662-672)
     const uint32_t* order = mov;
     if (gp.large_map) {
         int base = 0;
         for (int b = 0; b <= gp.n_sep; ++b) {
             const uint32_t want = b < gp.n_sep ? (uint32_t)b : kBucketBoundary;
-            for (int i0 = 0; i0 < n_mov; i0 += blockDim.x) {
+            for (int i0 = 0; i0 < n_mov; i0 += team_lanes<kW>()) {
                 const int i = i0 + TID;
                 const uint32_t ent = i < n_mov ? mov[i] : 0u;
                 const int f = i < n_mov && (ent & 0xFF) == want;
                 int tot;
-                const int r = block_scan_flag(f, sm.wave_tot, tot);
+                const int r = team_scan<kW>(f, sm.wave_tot, tot);
                 if (f) sorted[base + r] = ent;
                 base += tot;
             }
         }
-        __syncthreads();
+        psync<kW>();
         order = sorted;
     }
     par = par0 && (MFX_PAR_MASK & 2);
-    if (par && n_mov <= MFX_WAVE_STEP_MAX) {
-        if (TID < 64) move_parallel<true>(gp, sm, v, order, n_mov, *ps);
+    if (kW && par) {
+        move_parallel<true>(gp, sm, v, order, n_mov, ps);
+    } else if (par && n_mov <= MFX_WAVE_STEP_MAX) {
+        if (TID < 64) move_parallel<true>(gp, sm, v, order, n_mov, ps);
         __syncthreads();
     } else if (par) {
-        move_parallel<false>(gp, sm, v, order, n_mov, *ps);
+        move_parallel<false>(gp, sm, v, order, n_mov, ps);
     } else {
         if (TID == 0)
             for (int i = 0; i < n_mov; ++i) do_move_one(gp, sm, v, order[i]);
-        __syncthreads();
+        psync<kW>();
     }
     // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
     for (int r = 0; r < gp.n_rules; ++r) {
@@ -1048,8 +1078,8 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         int obj_recv = 0;
         for (int k = 0; k < R.n_recv; ++k) obj_recv |= R.recv_is_obj[k];
         if (TID == 0) sm.flags[r] = 0;
-        __syncthreads();
-        for (int i = TID; i < n; i += blockDim.x) {
+        psync<kW>();
+        for (int i = TID; i < n; i += team_lanes<kW>()) {
             const int id = v.grp_ids[R.subj_group * v.cap + i];
             const uint32_t m = v.meta[id];
             const int ob = v.op_obj[id];
@@ -1058,7 +1088,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
             for (int k = 0; k < R.n_recv; ++k)
                 if (!R.recv_is_obj[k]) v.next_r[id] += R.val[k];
         }
-        __syncthreads();
+        psync<kW>();
         if (obj_recv && TID == 0) {       // object receivers: DFS order, one lane
             for (int i = 0; i < n; ++i) {
                 const int id = v.grp_ids[R.subj_group * v.cap + i];
@@ -1069,7 +1099,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
                     if (R.recv_is_obj[k]) v.next_r[ob] += R.val[k];
             }
         }
-        __syncthreads();
+        psync<kW>();
     }
     // ---- done (GridWorld.cc:678-693)
     if (TID == 0) {
@@ -1079,7 +1109,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         for (int r = 0; r < gp.n_rules; ++r) d |= sm.flags[r] && gp.rules[r].terminal;
         done_out = d;
     }
-    __syncthreads();
+    psync<kW>();
 }
 
 // Copy an env into LDS, run the step, copy back.  When `lds` is 0 the env is worked on
@@ -1122,7 +1152,7 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     uint32_t rng = s.rng[e];
     int done = 0;
     load_serial_types(gp, sm);
-    step_env_core(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, nullptr, nid);
+    step_env_core<false>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, false, ParScratch{}, nid);
     if (lds) {
         for (int i = TID; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
         for (int i = TID; i < nid; i += blockDim.x) {
@@ -1141,18 +1171,19 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
 // ==================================================================================
 //  clear_dead (GridWorld.cc:696-728): ordered compaction + Agent::init_reward
 // ==================================================================================
+template <bool kW>
 __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v, int* wave_tot) {
     for (int g = 0; g < gp.n_groups; ++g) {
         const float step_reward = gp.type[g].step_reward;
         const int n = v.grp_n[g];
         int32_t* ids = v.grp_ids + g * v.cap;
         int base = 0;
-        for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+        for (int i0 = 0; i0 < n; i0 += team_lanes<kW>()) {
             const int i = i0 + TID;
             int id = -1, alive = 0;
             if (i < n) { id = ids[i]; alive = !meta_dead(v.meta[id]); }
             int tot;
-            const int r = block_scan_flag(alive, wave_tot, tot);
+            const int r = team_scan<kW>(alive, wave_tot, tot);
             // in-place compaction is safe: destination index <= source index, and all reads of
             // this round happened before the barrier inside block_scan_flag
             if (alive) {
@@ -1163,17 +1194,17 @@ __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v,
                 v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
             }
             base += tot;
-            __syncthreads();
+            psync<kW>();
         }
         if (TID == 0) { v.grp_n[g] = base; v.grp_dead[g] = 0; v.grp_reward[g] = 0.0f; }
-        __syncthreads();
+        psync<kW>();
     }
 }
 
 __global__ void __launch_bounds__(256) k_clear_dead(const GameParams* __restrict__ gp, State s) {
     __shared__ int wave_tot[16];
     EnvView v = global_view(s, blockIdx.x, gp->n_groups);
-    clear_dead_env(*gp, v, wave_tot);
+    clear_dead_env<false>(*gp, v, wave_tot);
 }
 
 // ==================================================================================
@@ -1533,6 +1564,64 @@ __device__ __forceinline__ void install_sync(const State& s, const PfTable& pt, 
         reinterpret_cast<uint32_t*>(&sc)[TID] = load_scalar_word(pt, e, TID);
 }
 
+// Policy, mean action, set_action, step, get_reward and clear_dead of one env, run by a team (see
+// psync): the whole workgroup, or wave 0 alone when the env has at most 64 agents.
+template <bool kB, bool kW>
+__device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s, const RolloutArgs& ra, EnvView& v,
+                                            EnvScalars& sc, int* misc, StepSmem& sm, int32_t* act, int* ahist,
+                                            uint32_t* atk, uint32_t* mov, uint32_t* sorted, float* red,
+                                            const ParScratch ps, int e, uint32_t step_index, int stamp_row,
+                                            uint32_t& rng, int& done, float& kills) {
+    (void)stamp_row;
+    const int G = gp.n_groups, cap = s.cap, acap = s.acap;
+    // ---------------- policy + mean action (former_act_prob), all groups in one pass
+    {
+        int ntot = 0;
+        for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+        for (int i = TID; i < G * 64; i += team_lanes<kW>()) ahist[i] = 0;
+        psync<kW>();
+        const uint32_t ekey = ra.policy_seed ^ mix32(step_index * 0x9E3779B9u + (uint32_t)e * 0x632BE5ABu);
+        for (int t = TID; t < ntot; t += team_lanes<kW>()) {
+            int g = 0, i = t;
+            while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
+            const int id = v.grp_ids[g * cap + i];
+            const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
+            const int a = rush_action(gp, v, g, id, key, ra.eps);
+            act[g * cap + i] = a;
+            if (i < ra.rowcap) ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
+            atomicAdd(&ahist[g * 64 + a], 1);
+        }
+        psync<kW>();
+        for (int t = TID; t < G * 64; t += team_lanes<kW>()) {
+            const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
+            if (k < na)   // empty group: np.mean of nothing is NaN
+                ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
+        }
+    }
+    MFX_TSTAMP(kW, 4);
+    // ---------------- set_action (group order) and step
+    for (int g = 0; g < G; ++g) set_action_group<kW>(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
+    MFX_TSTAMP(kW, 5);
+    step_env_core<kW>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, true, ps, sc.id_counter);
+    MFX_TSTAMP(kW, 6);
+    // ---------------- get_reward, episode return, kills
+    for (int g = 0; g < G; ++g) {
+        const int n = v.grp_n[g];
+        float part = 0.0f;
+        for (int i = TID; i < n; i += team_lanes<kW>()) {
+            const float r = v.next_r[v.grp_ids[g * cap + i]] + v.grp_reward[g];
+            if (i < ra.rowcap) ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
+            part += r;
+        }
+        const float tot = kW ? wave_sum(part) : block_sum(part, red);
+        if (TID == 0) { sc.ep_return[g] += tot; kills += (float)v.grp_dead[g]; }
+    }
+    MFX_TSTAMP(kW, 7);
+    // ---------------- clear_dead
+    clear_dead_env<kW>(gp, v, sm.wave_tot);
+    MFX_TSTAMP(kW, 8);
+}
+
 // One launch = one training-loop step for every env.  Persistent workgroups: the grid is what
 // fits on the chip at once, and each workgroup takes envs from a work queue, keeping env e in LDS
 // while the next env's image is already in flight into registers.
@@ -1645,56 +1734,24 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
         }
         __syncthreads();                       // the scratch region changes hands
         MFX_STAMP(3);
-        // ---------------- policy + mean action (former_act_prob), all groups in one pass
-        {
-            int ntot = 0;
-            for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
-            for (int i = TID; i < G * 64; i += blockDim.x) ahist[i] = 0;
-            __syncthreads();
-            const uint32_t ekey = ra.policy_seed ^ mix32(step_index * 0x9E3779B9u + (uint32_t)e * 0x632BE5ABu);
-            for (int t = TID; t < ntot; t += blockDim.x) {
-                int g = 0, i = t;
-                while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
-                const int id = v.grp_ids[g * cap + i];
-                const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
-                const int a = rush_action(gp, v, g, id, key, ra.eps);
-                act[g * cap + i] = a;
-                if (i < ra.rowcap) ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
-                atomicAdd(&ahist[g * 64 + a], 1);
-            }
-            __syncthreads();
-            for (int t = TID; t < G * 64; t += blockDim.x) {
-                const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
-                if (k < na)   // empty group: np.mean of nothing is NaN
-                    ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
-            }
-        }
-        MFX_STAMP(4);
-        // ---------------- set_action (group order) and step
-        for (int g = 0; g < G; ++g) set_action_group(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
-        MFX_STAMP(5);
+        // ---------------- policy, set_action, step, get_reward, clear_dead (agent_phase)
         uint32_t rng = sc.rng;
         int done = 0;
-        const ParScratch ps = carve_par(uni + u.par, acap, cap);
-        step_env_core(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, &ps, sc.id_counter);
-        MFX_STAMP(6);
-        // ---------------- get_reward, episode return, kills
         float kills = 0.0f;
-        for (int g = 0; g < G; ++g) {
-            const int n = v.grp_n[g];
-            float part = 0.0f;
-            for (int i = TID; i < n; i += blockDim.x) {
-                const float r = v.next_r[v.grp_ids[g * cap + i]] + v.grp_reward[g];
-                if (i < ra.rowcap) ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
-                part += r;
+        {
+            const ParScratch ps = carve_par(uni + u.par, acap, cap);
+            int ntot = 0;
+            for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+            if (ntot <= 64) {
+                if (TID < 64)
+                    agent_phase<kB, true>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, e,
+                                          step_index, stamp_row, rng, done, kills);
+                __syncthreads();
+            } else {
+                agent_phase<kB, false>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, e,
+                                       step_index, stamp_row, rng, done, kills);
             }
-            const float tot = block_sum(part, red);
-            if (TID == 0) { sc.ep_return[g] += tot; kills += (float)v.grp_dead[g]; }
         }
-        MFX_STAMP(7);
-        // ---------------- clear_dead
-        clear_dead_env(gp, v, sm.wave_tot);
-        MFX_STAMP(8);
         // ---------------- episode end -> reset + re-place the template (env.reset + add_agents)
         if (TID == 0) {
             sc.stats[3] += kills;
