@@ -645,6 +645,7 @@ __global__ void __launch_bounds__(256) k_set_action(const GameParams* __restrict
 struct SerialType {          // what the one-lane loops read per group, kept in LDS (the group
     float hp, damage, kill_supply, kill_reward, dead_penalty, attack_penalty;   // index is
     int attack_in_group, att_x_off, att_y_off, pad;                              // lane-varying:
+    int n_attack, turn_base, attack_base, n_action;
     int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];                       // from global it
     int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];                     // would be a vector
 };                                                                               // load per use)
@@ -668,6 +669,8 @@ __device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem
             S.hp = T.hp; S.damage = T.damage; S.kill_supply = T.kill_supply; S.kill_reward = T.kill_reward;
             S.dead_penalty = T.dead_penalty; S.attack_penalty = T.attack_penalty;
             S.attack_in_group = T.attack_in_group; S.att_x_off = T.att_x_off; S.att_y_off = T.att_y_off;
+            S.n_attack = T.n_attack; S.turn_base = T.turn_base; S.attack_base = T.attack_base;
+            S.n_action = T.n_action;
         }
     }
 }
@@ -1250,21 +1253,37 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {      // murmur3 finalize
 // Synthetic rush policy of SURVEY.md 8(d) (tests/battle_driver.rush_policy): attack the
 // first attack cell (index order = view2attack row-major order) holding an enemy, else move
 // 2 cells toward the map centre; with probability eps a uniform random action instead.
-__device__ __forceinline__ int rush_action(const GameParams& gp, const EnvView& v, int g, int id, uint32_t key,
-                                           float eps) {
-    const TypeParams& T = gp.type[g];
+// The synthetic rush policy: attack the first enemy among the attack cells in
+// view2attack order, else advance +-2 in x toward the centre; with probability eps a uniform
+// action.  The group index is lane-varying, so the type fields come from the LDS table, and the
+// attack cells are read 8 at a time (independent LDS reads instead of a dependent chain).
+__device__ __forceinline__ int rush_action(const GameParams& gp, const SerialType& S, const EnvView& v, int g,
+                                           int id, uint32_t key, float eps) {
     const uint32_t p = v.xy[id];
-    const int x = p & 0xFFFF, y = p >> 16;
-    int a = ((float)x / (float)gp.W < 0.5f) ? 8 : 4;
-    if (a >= T.turn_base) a = T.turn_base - 1;
-    for (int k = 0; k < T.n_attack; ++k) {
-        const int ox = x + T.att_x_off + T.att_dx[k], oy = y + T.att_y_off + T.att_dy[k];
-        if (ox < 0 || oy < 0 || ox >= gp.W || oy >= gp.H) continue;
-        const uint32_t c = v.cells[oy * gp.W + ox];
-        if (c < kCellWall && (int)meta_group(v.meta[c]) != g) { a = T.attack_base + k; break; }
+    const int x = p & 0xFFFF, y = p >> 16, W = gp.W, H = gp.H;
+    int a = ((float)x / (float)W < 0.5f) ? 8 : 4;
+    if (a >= S.turn_base) a = S.turn_base - 1;
+    const int bx = x + S.att_x_off, by = y + S.att_y_off, na = S.n_attack;
+    for (int k0 = 0; k0 < na; k0 += 8) {
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j;
+            const int ox = bx + S.att_dx[k], oy = by + S.att_dy[k];
+            const bool in = k < na && ox >= 0 && oy >= 0 && ox < W && oy < H;
+            const uint32_t cv = v.cells[in ? oy * W + ox : 0];
+            c[j] = in ? cv : kCellEmpty;
+        }
+        int hit = -1;
+#pragma unroll
+        for (int j = 7; j >= 0; --j) {
+            const uint32_t m = v.meta[c[j] < kCellWall ? c[j] : 0u];
+            if (c[j] < kCellWall && (int)meta_group(m) != g) hit = k0 + j;
+        }
+        if (hit >= 0) { a = S.attack_base + hit; break; }
     }
     const uint32_t h = mix32(key);
-    if ((float)(h >> 8) * (1.0f / 16777216.0f) < eps) a = (int)(mix32(h ^ 0x68E31DA4u) % (uint32_t)T.n_action);
+    if ((float)(h >> 8) * (1.0f / 16777216.0f) < eps) a = (int)(mix32(h ^ 0x68E31DA4u) % (uint32_t)S.n_action);
     return a;
 }
 
@@ -1586,14 +1605,14 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
             while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
             const int id = v.grp_ids[g * cap + i];
             const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
-            const int a = rush_action(gp, v, g, id, key, ra.eps);
+            const int a = rush_action(gp, sm.tt[g], v, g, id, key, ra.eps);
             act[g * cap + i] = a;
             if (i < ra.rowcap) ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
             atomicAdd(&ahist[g * 64 + a], 1);
         }
         psync<kW>();
         for (int t = TID; t < G * 64; t += team_lanes<kW>()) {
-            const int g = t >> 6, k = t & 63, na = gp.type[g].n_action, n = v.grp_n[g];
+            const int g = t >> 6, k = t & 63, na = sm.tt[g].n_action, n = v.grp_n[g];
             if (k < na)   // empty group: np.mean of nothing is NaN
                 ra.mean_act[((size_t)e * G + g) * na + k] = n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
         }
