@@ -1948,35 +1948,67 @@ hipError_t rollout_grid(const GameParams& gp, const State& s, int* grid) {
     return hipSuccess;
 }
 
-// Queue order of the next k_rollout launch: env indices by descending agent count (the cost of an
-// env's step grows with it), so the heaviest envs start first and the launch does not end on a
-// tail of a few late episode starts.  One workgroup; counting sort over the agent count.
-constexpr int kOrderBuckets = 1024;
+// Queue order of the next k_rollout launch: env indices heaviest first (an env's step time grows
+// with its agent count), so the launch does not end on a tail of a few late episode starts.
+// Eight weight classes, ranked with wave ballots (no atomics; the agent counts cluster on a few
+// values, which made an LDS-atomic histogram serialise); one workgroup, any E.
+constexpr int kOrderClasses = 8;
+
+__device__ __forceinline__ int env_weight_class(int w) {
+    return w >= 192 ? 0 : w >= 128 ? 1 : w >= 96 ? 2 : w >= 64 ? 3 : w >= 48 ? 4 : w >= 32 ? 5 : w >= 16 ? 6 : 7;
+}
 
 __global__ void __launch_bounds__(1024) k_env_order(const int32_t* __restrict__ grp_n, int E, int G,
                                                     int32_t* __restrict__ order) {
-    __shared__ int off[kOrderBuckets];
-    const int t = TID;
-    off[t] = 0;
-    __syncthreads();
-    auto bucket = [&](int e) {
+    __shared__ int base[kOrderClasses][16];
+    const int t = TID, lane = t & 63, wid = t >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int rounds = (E + 1023) / 1024;
+    auto cls_of = [&](int e) {
+        if (e >= E) return -1;
         int w = 0;
         for (int k = 0; k < G; ++k) w += grp_n[e * G + k];
-        return kOrderBuckets - 1 - min(max(w, 0), kOrderBuckets - 1);
+        return env_weight_class(w);
     };
-    for (int e = t; e < E; e += 1024) atomicAdd(&off[bucket(e)], 1);
-    __syncthreads();
-    for (int d = 1; d < kOrderBuckets; d <<= 1) {     // inclusive scan
-        const int x = t >= d ? off[t - d] : 0;
-        __syncthreads();
-        off[t] += x;
-        __syncthreads();
+    int cnt[kOrderClasses];
+#pragma unroll
+    for (int c = 0; c < kOrderClasses; ++c) cnt[c] = 0;
+    for (int j0 = 0; j0 < rounds; j0 += 16) {
+        int cl[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) cl[j] = cls_of((j0 + j) * 1024 + t);   // loads batched
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int c = 0; c < kOrderClasses; ++c) cnt[c] += __popcll(__ballot(cl[j] == c));
     }
-    const int excl = t ? off[t - 1] : 0;
+    if (lane == 0)
+        for (int c = 0; c < kOrderClasses; ++c) base[c][wid] = cnt[c];
     __syncthreads();
-    off[t] = excl;
+    if (t == 0) {                                      // class-major, then wave
+        int acc = 0;
+        for (int c = 0; c < kOrderClasses; ++c)
+            for (int w = 0; w < 16; ++w) { const int x = base[c][w]; base[c][w] = acc; acc += x; }
+    }
     __syncthreads();
-    for (int e = t; e < E; e += 1024) order[atomicAdd(&off[bucket(e)], 1)] = e;
+    int run[kOrderClasses];
+#pragma unroll
+    for (int c = 0; c < kOrderClasses; ++c) run[c] = base[c][wid];
+    for (int j0 = 0; j0 < rounds; j0 += 16) {
+        int cl[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) cl[j] = cls_of((j0 + j) * 1024 + t);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int e = (j0 + j) * 1024 + t;
+#pragma unroll
+            for (int c = 0; c < kOrderClasses; ++c) {
+                const unsigned long long m = __ballot(cl[j] == c);
+                if (cl[j] == c) order[run[c] + __popcll(m & lt)] = e;
+                run[c] += __popcll(m);
+            }
+        }
+    }
 }
 
 hipError_t launch_env_order(const State& s, int G, int32_t* d_order, hipStream_t st) {

@@ -79,3 +79,22 @@ def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps):
                 env.add_agents(h[0], method="custom", pos=left)
                 env.add_agents(h[1], method="custom", pos=right)
         del env
+
+
+def test_rollout_processes_every_env_once():
+    """The persistent work queue (k_env_order + per-launch counters) hands every env to exactly one
+    workgroup per launch: before the armies meet no agent dies, so each env's agent-step counter
+    must read 256 * steps.  E is not a multiple of the order kernel's 1024-env rounds."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, steps = 5003, 3
+    left, right = bd.block_positions(64, 128)
+    eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=400, eps=0.0, seed=7, stagger=False)
+    grid, lds = eng.rollout_info()
+    assert 0 < grid <= E and lds > 0
+    eng.rollout_step(steps)
+    got = torch.empty(E, dtype=torch.int64)
+    eng.rollout_copy("agent_steps", got)
+    eng.sync()
+    assert (got == 256 * steps).all(), np.unique(got.numpy())
