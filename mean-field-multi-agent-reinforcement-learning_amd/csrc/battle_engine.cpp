@@ -133,7 +133,8 @@ public:
     DevBuf<double> ro_mean, ro_stats;
     DevBuf<unsigned long long> ro_steps;
     DevBuf<int32_t> ro_work;                 // k_rollout work-queue counters (2)
-    DevBuf<int32_t> ro_order;                // k_rollout queue order (k_env_order)
+    DevBuf<int32_t> ro_cls_cnt, ro_cls_list; // k_rollout work queue (weight-class lists)
+    uint64_t ro_launch = 0;                  // launches so far (queue phase = ro_launch % 6)
     DevBuf<uint4> ro_image;                  // reset image (k_reset_image)
     DevBuf<RolloutCtx> ro_ctx;               // device copy of {s, ra} read by k_rollout
     RolloutCtx ro_ctx_host{};
@@ -528,8 +529,17 @@ public:
             ro_work.ensure(2);
             MFX_HIP_THROW(hipMemsetAsync(ro_work.p, 0, 2 * sizeof(int32_t), stream));
             ro_image.ensure((rollout_reset_image_bytes(gp, s.cells_n, s.cap) + 15) / 16);
-            ro_order.ensure(E);
-            ra.work = ro_work.p; ra.work_sel = 0; ra.reset_image = ro_image.p; ra.order = ro_order.p;
+            // queue for the next launch: every env in class 0 in index order, other counts zero
+            ro_cls_cnt.ensure(3 * 8); ro_cls_list.ensure((size_t)2 * 8 * E);
+            const int qp = (int)(ro_launch % 6);
+            std::vector<int32_t> cnt(3 * 8, 0), idx((size_t)E);
+            cnt[(qp % 3) * 8] = E;
+            for (int e = 0; e < E; e++) idx[e] = e;
+            MFX_HIP_THROW(hipMemcpy(ro_cls_cnt.p, cnt.data(), sizeof(int32_t) * cnt.size(), hipMemcpyHostToDevice));
+            MFX_HIP_THROW(hipMemcpy(ro_cls_list.p + (size_t)(qp & 1) * 8 * E, idx.data(), sizeof(int32_t) * E,
+                                    hipMemcpyHostToDevice));
+            ra.work = ro_work.p; ra.work_sel = 0; ra.reset_image = ro_image.p;
+            ra.cls_cnt = ro_cls_cnt.p; ra.cls_list = ro_cls_list.p; ra.cls_stride = E;
             MFX_HIP_THROW(launch_reset_image(gp, d_gp, s, ra, ro_image.p, stream));
             MFX_HIP_THROW(rollout_grid(gp, s, &ro_grid));
             ro_cap = s.cap;
@@ -547,8 +557,9 @@ public:
         if (!rollout_ready) return fail("rollout_step before rollout_init");
         if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
         for (int i = 0; i < n_steps; i++) {
-            MFX_HIP(launch_env_order(s, n_groups(), ro_order.p, stream));
-            MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.step_index, ra.work_sel, ro_grid, stream));
+            MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.step_index, ra.work_sel, (int)(ro_launch % 6), ro_grid,
+                                   stream));
+            ro_launch++;
             ra.step_index++;
             ra.work_sel ^= 1;
         }

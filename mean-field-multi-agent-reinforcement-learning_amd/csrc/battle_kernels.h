@@ -24,8 +24,7 @@ hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t
 hipError_t set_stamp_buffer(unsigned long long* d_buf);
 size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap);
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                          uint32_t step_index, int work_sel, int grid, hipStream_t st);
-hipError_t launch_env_order(const State& s, int G, int32_t* d_order, hipStream_t st);
+                          uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st);
 hipError_t rollout_grid(const GameParams& gp, const State& s, int* grid);
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap);
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,

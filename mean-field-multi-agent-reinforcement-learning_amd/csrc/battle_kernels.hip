@@ -96,10 +96,10 @@ struct EnvView {
     float* hp;
     float* next_r;
     float* last_r;
-    int32_t* last_act;
+    uint8_t* last_act;
     int32_t* op_obj;
     uint8_t* meta;
-    int32_t* grp_ids;      // [G][cap]
+    uint16_t* grp_ids;     // [G][cap]
     int32_t* grp_n;        // [G]
     int32_t* grp_dead;     // [G]
     float* grp_reward;     // [G]
@@ -176,7 +176,7 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
         v.op_obj[id] = -1;
         v.meta[id] = (uint8_t)meta_make(0, kOpNull, group);
         int& n = v.grp_n[group];
-        v.grp_ids[group * s.cap + n] = id;
+        v.grp_ids[group * s.cap + n] = (uint16_t)id;
         ++n;
     };
     if (method == 0) {
@@ -271,7 +271,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     const int NV = VW * VH, VF = NV * NC;
     const bool MM = kB ? true : gp.minimap != 0;
     const int per = MM ? 3 : 2;
-    const int32_t* ids = v.grp_ids + g * v.cap;
+    const uint16_t* ids = v.grp_ids + g * v.cap;
     // ---- phase 1: one lane per (agent, view cell) computes that cell's NC channels
     for (int p = TID; p < k * NV; p += blockDim.x) {
         const int al = p / NV, c = p - al * NV;
@@ -356,7 +356,7 @@ constexpr int kWaveStageFloats = kWaveCells * BattleShape::NC;   // 448 floats =
 __device__ __forceinline__ void obs_agent_records(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int g,
                                                   int n) {
     const TypeParams& T = gp.type[g];
-    const int32_t* ids = v.grp_ids + g * v.cap;
+    const uint16_t* ids = v.grp_ids + g * v.cap;
     for (int a = TID; a < n; a += blockDim.x) {
         const int id = ids[a];
         const uint32_t p = v.xy[id];
@@ -460,7 +460,7 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
     const int lane = TID & 63, wid = TID >> 6, nw = blockDim.x >> 6;
     const int W = gp.W, H = gp.H;
     const TypeParams& T = gp.type[g];
-    const int32_t* ids = v.grp_ids + g * v.cap;
+    const uint16_t* ids = v.grp_ids + g * v.cap;
     const float* mm_own = sm.mm + g * NV;
     const float* mm_en = sm.mm + (g ^ 1) * NV;
     float* st = wave_stage + wid * kWaveStageFloats;
@@ -1179,7 +1179,7 @@ __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v,
     for (int g = 0; g < gp.n_groups; ++g) {
         const float step_reward = gp.type[g].step_reward;
         const int n = v.grp_n[g];
-        int32_t* ids = v.grp_ids + g * v.cap;
+        uint16_t* ids = v.grp_ids + g * v.cap;
         int base = 0;
         for (int i0 = 0; i0 < n; i0 += team_lanes<kW>()) {
             const int i = i0 + TID;
@@ -1190,7 +1190,7 @@ __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v,
             // in-place compaction is safe: destination index <= source index, and all reads of
             // this round happened before the barrier inside block_scan_flag
             if (alive) {
-                ids[base + r] = id;
+                ids[base + r] = (uint16_t)id;
                 v.last_r[id] = v.next_r[id];
                 v.next_r[id] = step_reward;
                 v.op_obj[id] = -1;
@@ -1220,7 +1220,7 @@ __global__ void __launch_bounds__(256) k_get(const GameParams* __restrict__ gp, 
     const int n = v.grp_n[g];
     if (what == kGetNum) { if (TID == 0) reinterpret_cast<int*>(out)[e] = n; return; }
     if (n > rowcap) { if (TID == 0) set_err(s, 4); return; }
-    const int32_t* ids = v.grp_ids + g * v.cap;
+    const uint16_t* ids = v.grp_ids + g * v.cap;
     const size_t o = (size_t)e * rowcap;
     for (int i = TID; i < n; i += blockDim.x) {
         const int id = ids[i];
@@ -1332,7 +1332,7 @@ __host__ __device__ inline size_t rollout_scratch_bytes(const GameParams& gp, in
 // same layout is used for the reset image in HBM (RolloutArgs::reset_image).
 __host__ __device__ inline size_t env_image_bytes(int cells_n, int cap, int G) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    return r16((size_t)cells_n * 2) + 6 * r16((size_t)cap * 4) + r16(cap) + r16((size_t)G * cap * 4);
+    return r16((size_t)cells_n * 2) + 5 * r16((size_t)cap * 4) + 2 * r16(cap) + r16((size_t)G * cap * 2);
 }
 
 size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
@@ -1354,10 +1354,10 @@ __device__ __forceinline__ EnvView carve_env(char* base, int cells_n, int cap, i
     v.hp = reinterpret_cast<float*>(carve((size_t)cap * 4));
     v.next_r = reinterpret_cast<float*>(carve((size_t)cap * 4));
     v.last_r = reinterpret_cast<float*>(carve((size_t)cap * 4));
-    v.last_act = reinterpret_cast<int32_t*>(carve((size_t)cap * 4));
     v.op_obj = reinterpret_cast<int32_t*>(carve((size_t)cap * 4));
+    v.last_act = reinterpret_cast<uint8_t*>(carve((size_t)cap));
     v.meta = reinterpret_cast<uint8_t*>(carve((size_t)cap));
-    v.grp_ids = reinterpret_cast<int32_t*>(carve((size_t)G * cap * 4));
+    v.grp_ids = reinterpret_cast<uint16_t*>(carve((size_t)G * cap * 2));
     return v;
 }
 
@@ -1398,7 +1398,7 @@ __global__ void __launch_bounds__(256) k_reset_image(const GameParams* __restric
                 v.hp[id] = T.hp; v.last_r[id] = 0.0f; v.next_r[id] = T.step_reward;
                 v.last_act[id] = T.n_action; v.op_obj[id] = -1;
                 v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
-                v.grp_ids[g * cap + scal[g]++] = id;
+                v.grp_ids[g * cap + scal[g]++] = (uint16_t)id;
             }
         }
         scal[4] = idc;
@@ -1426,18 +1426,20 @@ struct EnvScalars {
 constexpr int kScalarWords = 30;
 
 // Register prefetch of one env (k_rollout fast path): while env e is processed, every lane of
-// waves 0-2 holds its share of env e+1's image (3 + 3 rows of 16 B; wave 0 also one scalar word),
+// waves 0-2 holds its share of env e+1's image (up to 5 rows of 16 B; wave 0 also one scalar word),
 // so the next install is LDS stores only.  Wave 3 alone writes env e back: a wave's vmcnt is in
 // order, so the prefetch waves must not have the write-back stores queued ahead of their loads.
-// The 16-B rows of the per-id arrays and group lists are numbered in LDS order:
-// [xy hp next_r last_r last_act op_obj] (c4 = cap/4 rows each), [meta] (c4/4), [grp_ids] (G*c4).
+// The image's 16-B rows are numbered in LDS order: the cells (nc16 rows), then
+// [xy hp next_r last_r op_obj] (c4 = cap/4 rows each), [last_act] [meta] (c4/4 each), [grp_ids] (G*c4/2).
 constexpr int kPfLanes = 192;                     // waves 0-2
-constexpr int kPfCellRows = 3 * kPfLanes;
-constexpr int kPfSmallRows = 3 * kPfLanes;
+constexpr int kPfSlots = 5;
+constexpr int kPfRows = kPfSlots * kPfLanes;
 constexpr int kWbWave = 3;                        // the write-back wave
 
+__host__ __device__ inline int image_small_rows(int c4, int G) { return 5 * c4 + 2 * (c4 >> 2) + G * (c4 >> 1); }
+
 struct EnvPrefetch {
-    uint4 c0, c1, c2, a0, a1, a2;
+    uint4 r[kPfSlots];
     uint32_t w;
 };
 
@@ -1447,7 +1449,7 @@ struct EnvPrefetch {
 // separate pointers per lane instead would serialise the loads (each predicated load into the same
 // registers waits for the previous one).
 struct PfTable {
-    unsigned long long base[8];
+    unsigned long long base[8];         // xy hp next_r last_r op_obj, last_act, meta, grp_ids
     unsigned int stride[8];
     unsigned long long sbase[32];       // 0: word absent (group >= G, padding)
     unsigned int sstride[32];
@@ -1463,10 +1465,10 @@ __device__ __forceinline__ void pf_table_init(PfTable& pt, const State& s, const
         if (t == 1) p = s.hp;
         if (t == 2) p = s.next_r;
         if (t == 3) p = s.last_r;
-        if (t == 4) p = s.last_act;
-        if (t == 5) p = s.op_obj;
+        if (t == 4) p = s.op_obj;
+        if (t == 5) { p = s.last_act; st = (unsigned)s.cap; }
         if (t == 6) { p = s.meta; st = (unsigned)s.cap; }
-        if (t == 7) { p = s.grp_ids; st = cap4 * (unsigned)G; }
+        if (t == 7) { p = s.grp_ids; st = (unsigned)s.cap * 2u * (unsigned)G; }
         pt.base[t] = (unsigned long long)p;
         pt.stride[t] = st;
     }
@@ -1503,12 +1505,19 @@ __device__ __forceinline__ uint4 ld_g16(const g_u32x4* p) {
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
-// Address of 16-B row k of the small region of env e (LDS order, see EnvPrefetch).
+// Address of 16-B row k of the per-id / group-list part of env e's image (LDS order, see EnvPrefetch).
 __device__ __forceinline__ const g_u32x4* small_row_addr(const PfTable& pt, int e, int k, int sh, int c4) {
-    const int j = k >> sh, k2 = k - 6 * c4, mrows = c4 >> 2;
-    const int a = j < 6 ? j : (k2 < mrows ? 6 : 7);
-    const int r = j < 6 ? (k & (c4 - 1)) : (k2 < mrows ? k2 : k2 - mrows);
+    const int j = k >> sh, k2 = k - 5 * c4, q = c4 >> 2;
+    const int a = j < 5 ? j : (k2 < q ? 5 : (k2 < 2 * q ? 6 : 7));
+    const int r = j < 5 ? (k & (c4 - 1)) : (k2 < q ? k2 : (k2 < 2 * q ? k2 - q : k2 - 2 * q));
     return (const g_u32x4*)(pt.base[a] + (unsigned long long)e * pt.stride[a] + (unsigned)r * 16u);
+}
+
+// Address of row r of env e's whole image: the cells first, then the small part.
+__device__ __forceinline__ const g_u32x4* image_row_addr(const PfTable& pt, const State& s, int e, int r, int nc16,
+                                                         int sh, int c4) {
+    const unsigned long long cells = (unsigned long long)(s.cells + (size_t)e * s.cells_n) + (unsigned)r * 16u;
+    return r < nc16 ? (const g_u32x4*)cells : small_row_addr(pt, e, r - nc16, sh, c4);
 }
 
 __device__ __forceinline__ g_u32* scalar_addr(const PfTable& pt, int e, int w) {
@@ -1521,36 +1530,31 @@ __device__ __forceinline__ uint32_t load_scalar_word(const PfTable& pt, int e, i
     return p ? *p : 0u;
 }
 
-__device__ __forceinline__ void pf_issue(EnvPrefetch& pf, const PfTable& pt, const State& s, int e, int nc16,
-                                         int ns16, int sh, int c4) {
+__device__ __forceinline__ void pf_issue(EnvPrefetch& pf, const PfTable& pt, const State& s, int e, int nrows,
+                                         int nc16, int sh, int c4) {
     const int t = TID;
     if (t >= kPfLanes) return;
-    const uint4* gc = reinterpret_cast<const uint4*>(s.cells + (size_t)e * s.cells_n);
-    if (t < nc16) pf.c0 = gc[t];
-    if (t + kPfLanes < nc16) pf.c1 = gc[t + kPfLanes];
-    if (t + 2 * kPfLanes < nc16) pf.c2 = gc[t + 2 * kPfLanes];
-    if (t < ns16) pf.a0 = ld_g16(small_row_addr(pt, e, t, sh, c4));
-    if (t + kPfLanes < ns16) pf.a1 = ld_g16(small_row_addr(pt, e, t + kPfLanes, sh, c4));
-    if (t + 2 * kPfLanes < ns16) pf.a2 = ld_g16(small_row_addr(pt, e, t + 2 * kPfLanes, sh, c4));
+#pragma unroll
+    for (int j = 0; j < kPfSlots; ++j) {
+        const int r = t + j * kPfLanes;
+        if (r < nrows) pf.r[j] = ld_g16(image_row_addr(pt, s, e, r, nc16, sh, c4));
+    }
     if (t < kScalarWords) pf.w = load_scalar_word(pt, e, t);
 }
 
-__device__ __forceinline__ void pf_install(const EnvPrefetch& pf, const EnvView& v, EnvScalars& sc, int nc16,
-                                           int ns16) {
+__device__ __forceinline__ void pf_install(const EnvPrefetch& pf, char* image, EnvScalars& sc, int nrows) {
     // One unconditional vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  Left to the
     // compiler, the waits sit inside the exec-masked stores below, so along the skipped paths the
     // registers still look in flight and the next pf_issue waits again before every load.
     __builtin_amdgcn_s_waitcnt(0x0F70);
     const int t = TID;
     if (t >= kPfLanes) return;
-    uint4* lc = reinterpret_cast<uint4*>(v.cells);
-    uint4* la = reinterpret_cast<uint4*>(v.xy);
-    if (t < nc16) lc[t] = pf.c0;
-    if (t + kPfLanes < nc16) lc[t + kPfLanes] = pf.c1;
-    if (t + 2 * kPfLanes < nc16) lc[t + 2 * kPfLanes] = pf.c2;
-    if (t < ns16) la[t] = pf.a0;
-    if (t + kPfLanes < ns16) la[t + kPfLanes] = pf.a1;
-    if (t + 2 * kPfLanes < ns16) la[t + 2 * kPfLanes] = pf.a2;
+    uint4* d = reinterpret_cast<uint4*>(image);
+#pragma unroll
+    for (int j = 0; j < kPfSlots; ++j) {
+        const int r = t + j * kPfLanes;
+        if (r < nrows) d[r] = pf.r[j];
+    }
     if (t < kScalarWords) reinterpret_cast<uint32_t*>(&sc)[t] = pf.w;
 }
 
@@ -1575,12 +1579,48 @@ __device__ __forceinline__ void install_sync(const State& s, const PfTable& pt, 
     copy16(v.hp, gv.hp, (size_t)cap * 4);
     copy16(v.next_r, gv.next_r, (size_t)cap * 4);
     copy16(v.last_r, gv.last_r, (size_t)cap * 4);
-    copy16(v.last_act, gv.last_act, (size_t)cap * 4);
     copy16(v.op_obj, gv.op_obj, (size_t)cap * 4);
+    copy16(v.last_act, gv.last_act, (size_t)cap);
     copy16(v.meta, gv.meta, (size_t)cap);
-    copy16(v.grp_ids, gv.grp_ids, (size_t)G * cap * 4);
+    copy16(v.grp_ids, gv.grp_ids, (size_t)G * cap * 2);
     if (TID < kScalarWords)
         reinterpret_cast<uint32_t*>(&sc)[TID] = load_scalar_word(pt, e, TID);
+}
+
+// Work queue of k_rollout: envs heaviest first (an env's step time grows with its agent count), so
+// a launch does not end on a tail of a few late episode starts.  Every workgroup files the envs it
+// finishes under their new weight class in the next launch's class lists (buffered in LDS, one
+// atomic per class per flush); the next launch walks the lists class by class.
+constexpr int kOrderClasses = 8;
+
+__device__ __forceinline__ int env_weight_class(int w) {
+    return w >= 192 ? 0 : w >= 128 ? 1 : w >= 96 ? 2 : w >= 64 ? 3 : w >= 48 ? 4 : w >= 32 ? 5 : w >= 16 ? 6 : 7;
+}
+
+
+
+constexpr int kQueueBuf = 32;                      // envs buffered per workgroup before a flush
+
+// Env at queue position i of this launch (qpre: prefix of the class counts, qpre[8] = E).
+__device__ __forceinline__ int queue_env(const RolloutArgs& ra, const int* qpre, int i, int E, int qphase) {
+    if (i >= E) return E;
+    int c = 0;
+    while (c < kOrderClasses - 1 && i >= qpre[c + 1]) ++c;
+    return ra.cls_list[((size_t)(qphase & 1) * kOrderClasses + c) * ra.cls_stride + (i - qpre[c])];
+}
+
+// Thread 0: append the buffered envs to the next launch's class lists.
+__device__ __forceinline__ void queue_flush(const RolloutArgs& ra, const int* wg_env, const uint8_t* wg_cls, int n,
+                                            int qphase, int* tmp) {
+    const int cn = (qphase + 1) % 3, ln = (qphase + 1) & 1;
+    for (int c = 0; c < kOrderClasses; ++c) tmp[c] = 0;
+    for (int k = 0; k < n; ++k) ++tmp[wg_cls[k]];
+    for (int c = 0; c < kOrderClasses; ++c)
+        tmp[c] = tmp[c] ? atomicAdd(ra.cls_cnt + cn * kOrderClasses + c, tmp[c]) : 0;
+    for (int k = 0; k < n; ++k) {
+        const int c = wg_cls[k];
+        ra.cls_list[((size_t)ln * kOrderClasses + c) * ra.cls_stride + tmp[c]++] = wg_env[k];
+    }
 }
 
 // Policy, mean action, set_action, step, get_reward and clear_dead of one env, run by a team (see
@@ -1647,42 +1687,51 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
 template <bool kB, bool kPf>
 __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GameParams* __restrict__ gpp,
                                                                  const RolloutCtx* __restrict__ ctx,
-                                                                 uint32_t step_index, int work_sel) {
+                                                                 uint32_t step_index, int work_sel, int qphase) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ StepSmem sm;
     __shared__ EnvScalars sc;
     __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 3 episode end, 4 done, 5-7 queue hand-off
     __shared__ int32_t n_before[kMaxGroups];
     __shared__ PfTable pt;
-    // Work queue: position i of this launch is env ra.order[i] (heaviest envs first, k_env_order).
+    __shared__ int qpre[kOrderClasses + 1], qtmp[kOrderClasses];
+    __shared__ int wg_env[kQueueBuf];
+    __shared__ uint8_t wg_cls[kQueueBuf];
+    __shared__ int wg_n;                     // envs buffered in wg_env / wg_cls
+    // Work queue: position i of this launch is env queue_env(i) (class lists, heaviest first).
     // The hand-off is pipelined so that no queue access is waited on: while env e_k is processed,
     // e_{k+1} is being prefetched, thread 0 holds e_{k+2} (o) and the queue slot of e_{k+3} (g),
     // and both loads land before the next install's vmcnt(0).
     int e, en;
     int o = 0, g = 0;
     EnvPrefetch pf;
-    pf.c0 = pf.c1 = pf.c2 = pf.a0 = pf.a1 = pf.a2 = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < kPfSlots; ++j) pf.r[j] = make_uint4(0, 0, 0, 0);
     pf.w = 0;
     {
         const GameParams& gp = kconst(gpp);
         const State& s = kconst(ctx).s;
         const RolloutArgs& ra = kconst(ctx).ra;
         const int G = gp.n_groups, c4 = s.cap >> 2, sh = __ffs(c4) - 1;
-        const int nc16 = s.cells_n >> 3, ns16 = 6 * c4 + (c4 >> 2) + G * c4;
+        const int nc16 = s.cells_n >> 3, nrows = nc16 + image_small_rows(c4, G);
         if (TID == 0) {
-            if (blockIdx.x == 0) ra.work[work_sel ^ 1] = 0;
-            for (int k = 5; k < 8; ++k) {
-                const int i = atomicAdd(ra.work + work_sel, 1);
-                misc[k] = i < s.E ? ra.order[i] : s.E;
+            if (blockIdx.x == 0) {
+                ra.work[work_sel ^ 1] = 0;
+                for (int c = 0; c < kOrderClasses; ++c) ra.cls_cnt[((qphase + 2) % 3) * kOrderClasses + c] = 0;
             }
+            int acc = 0;
+            for (int c = 0; c < kOrderClasses; ++c) { qpre[c] = acc; acc += ra.cls_cnt[(qphase % 3) * kOrderClasses + c]; }
+            qpre[kOrderClasses] = acc;
+            for (int k = 5; k < 8; ++k) misc[k] = queue_env(ra, qpre, atomicAdd(ra.work + work_sel, 1), s.E, qphase);
             g = atomicAdd(ra.work + work_sel, 1);
+            wg_n = 0;
         }
         load_serial_types(gp, sm);
         pf_table_init(pt, s, ra, G);
         __syncthreads();
         e = misc[5]; en = misc[6];
         if (TID == 0) o = misc[7];
-        if (kPf && e < s.E) pf_issue(pf, pt, s, e, nc16, ns16, sh, c4);
+        if (kPf && e < s.E) pf_issue(pf, pt, s, e, nrows, nc16, sh, c4);
     }
     while (true) {
 #ifdef MFX_STAMPS
@@ -1712,21 +1761,21 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
     const size_t img_bytes = env_image_bytes(s.cells_n, cap, G);
     const int32_t* img_scal = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(ra.reset_image) + img_bytes);
     const int c4 = cap >> 2, sh = __ffs(c4) - 1;
-    const int nc16 = s.cells_n >> 3, ns16 = 6 * c4 + (c4 >> 2) + G * c4;
+    const int nc16 = s.cells_n >> 3, nrows = nc16 + image_small_rows(c4, G);
     {
         const int stamp_row = e;
         (void)stamp_row;
         MFX_STAMP(0);
         // ---------------- install env e
-        if (kPf) pf_install(pf, v, sc, nc16, ns16);
+        if (kPf) pf_install(pf, smem, sc, nrows);
         else install_sync(s, pt, e, G, v, sc);
         if (TID == 0) { misc[0] = 0; misc[1] = 0; misc[5] = o; }
         __syncthreads();
         MFX_STAMP(13);
         if (TID < G) n_before[TID] = sc.grp_n[TID];
-        if (kPf && en < s.E) pf_issue(pf, pt, s, en, nc16, ns16, sh, c4);
+        if (kPf && en < s.E) pf_issue(pf, pt, s, en, nrows, nc16, sh, c4);
         if (TID == 0) {                        // lands long before the next install
-            o = g < s.E ? ra.order[g] : s.E;
+            o = queue_env(ra, qpre, g, s.E, qphase);
             g = atomicAdd(ra.work + work_sel, 1);
         }
         MFX_STAMP(1);
@@ -1803,6 +1852,13 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
             __syncthreads();
         }
         MFX_STAMP(9);
+        if (TID == 0) {                        // file the env for the next launch's queue
+            int w = 0;
+            for (int q = 0; q < G; ++q) w += sc.grp_n[q];
+            wg_env[wg_n] = e;
+            wg_cls[wg_n] = (uint8_t)env_weight_class(w);
+            if (++wg_n == kQueueBuf) { queue_flush(ra, wg_env, wg_cls, wg_n, qphase, qtmp); wg_n = 0; }
+        }
         // ---------------- write the env back (wave kWbWave only, see EnvPrefetch)
         if ((TID >> 6) == kWbWave) {
             const int lane = TID & 63;
@@ -1818,11 +1874,11 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
             wcopy16(gv.hp, v.hp, n4 * 4, lane);
             wcopy16(gv.next_r, v.next_r, n4 * 4, lane);
             wcopy16(gv.last_r, v.last_r, n4 * 4, lane);
-            wcopy16(gv.last_act, v.last_act, n4 * 4, lane);
             wcopy16(gv.op_obj, v.op_obj, n4 * 4, lane);
+            wcopy16(gv.last_act, v.last_act, n16, lane);
             wcopy16(gv.meta, v.meta, n16, lane);
             for (int g = 0; g < G; ++g)
-                wcopy16(gv.grp_ids + g * cap, v.grp_ids + g * cap, (((size_t)v.grp_n[g] + 3) & ~(size_t)3) * 4, lane);
+                wcopy16(gv.grp_ids + g * cap, v.grp_ids + g * cap, (((size_t)v.grp_n[g] + 7) & ~(size_t)7) * 2, lane);
             if (lane < kScalarWords) {
                 g_u32* p = scalar_addr(pt, e, lane);
                 if (p) *p = reinterpret_cast<const uint32_t*>(&sc)[lane];
@@ -1835,6 +1891,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
         en = misc[5];
     }
     }
+    if (TID == 0 && wg_n) queue_flush(kconst(ctx).ra, wg_env, wg_cls, wg_n, qphase, qtmp);
 }
 
 // ==================================================================================
@@ -1908,8 +1965,8 @@ hipError_t set_stamp_buffer(unsigned long long* d_buf) {
 
 // The register-prefetch instance needs the env image to fit the prefetch lanes (see EnvPrefetch).
 static bool rollout_prefetch_ok(const GameParams& gp, const State& s) {
-    const int c4 = s.cap >> 2, nc16 = s.cells_n >> 3, ns16 = 6 * c4 + (c4 >> 2) + gp.n_groups * c4;
-    return (s.cells_n & 7) == 0 && nc16 <= kPfCellRows && ns16 <= kPfSmallRows;
+    const int c4 = s.cap >> 2, nc16 = s.cells_n >> 3;
+    return (s.cells_n & 7) == 0 && nc16 + image_small_rows(c4, gp.n_groups) <= kPfRows;
 }
 
 template <class F>
@@ -1922,11 +1979,11 @@ static hipError_t with_rollout_kernel(const GameParams& gp, const State& s, F&& 
 }
 
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                          uint32_t step_index, int work_sel, int grid, hipStream_t st) {
+                          uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st) {
     const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     return with_rollout_kernel(gp, s, [&](auto kern) {
-        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel);
+        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel, qphase);
         return hipGetLastError();
     });
 }
@@ -1946,74 +2003,6 @@ hipError_t rollout_grid(const GameParams& gp, const State& s, int* grid) {
     const long long want = (long long)cus * (per_cu > 0 ? per_cu : 1);
     *grid = (int)(want < s.E ? want : s.E);
     return hipSuccess;
-}
-
-// Queue order of the next k_rollout launch: env indices heaviest first (an env's step time grows
-// with its agent count), so the launch does not end on a tail of a few late episode starts.
-// Eight weight classes, ranked with wave ballots (no atomics; the agent counts cluster on a few
-// values, which made an LDS-atomic histogram serialise); one workgroup, any E.
-constexpr int kOrderClasses = 8;
-
-__device__ __forceinline__ int env_weight_class(int w) {
-    return w >= 192 ? 0 : w >= 128 ? 1 : w >= 96 ? 2 : w >= 64 ? 3 : w >= 48 ? 4 : w >= 32 ? 5 : w >= 16 ? 6 : 7;
-}
-
-__global__ void __launch_bounds__(1024) k_env_order(const int32_t* __restrict__ grp_n, int E, int G,
-                                                    int32_t* __restrict__ order) {
-    __shared__ int base[kOrderClasses][16];
-    const int t = TID, lane = t & 63, wid = t >> 6;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    const int rounds = (E + 1023) / 1024;
-    auto cls_of = [&](int e) {
-        if (e >= E) return -1;
-        int w = 0;
-        for (int k = 0; k < G; ++k) w += grp_n[e * G + k];
-        return env_weight_class(w);
-    };
-    int cnt[kOrderClasses];
-#pragma unroll
-    for (int c = 0; c < kOrderClasses; ++c) cnt[c] = 0;
-    for (int j0 = 0; j0 < rounds; j0 += 16) {
-        int cl[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) cl[j] = cls_of((j0 + j) * 1024 + t);   // loads batched
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-#pragma unroll
-            for (int c = 0; c < kOrderClasses; ++c) cnt[c] += __popcll(__ballot(cl[j] == c));
-    }
-    if (lane == 0)
-        for (int c = 0; c < kOrderClasses; ++c) base[c][wid] = cnt[c];
-    __syncthreads();
-    if (t == 0) {                                      // class-major, then wave
-        int acc = 0;
-        for (int c = 0; c < kOrderClasses; ++c)
-            for (int w = 0; w < 16; ++w) { const int x = base[c][w]; base[c][w] = acc; acc += x; }
-    }
-    __syncthreads();
-    int run[kOrderClasses];
-#pragma unroll
-    for (int c = 0; c < kOrderClasses; ++c) run[c] = base[c][wid];
-    for (int j0 = 0; j0 < rounds; j0 += 16) {
-        int cl[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) cl[j] = cls_of((j0 + j) * 1024 + t);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int e = (j0 + j) * 1024 + t;
-#pragma unroll
-            for (int c = 0; c < kOrderClasses; ++c) {
-                const unsigned long long m = __ballot(cl[j] == c);
-                if (cl[j] == c) order[run[c] + __popcll(m & lt)] = e;
-                run[c] += __popcll(m);
-            }
-        }
-    }
-}
-
-hipError_t launch_env_order(const State& s, int G, int32_t* d_order, hipStream_t st) {
-    k_env_order<<<1, 1024, 0, st>>>(s.grp_n, s.E, G, d_order);
-    return hipGetLastError();
 }
 
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,

@@ -10,11 +10,11 @@
 //     hp        f32 [E][cap]
 //     next_r    f32 [E][cap]   Agent::next_reward  (GridWorld.h:248)
 //     last_r    f32 [E][cap]   Agent::last_reward
-//     last_act  i32 [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145)
+//     last_act  u8  [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145)
 //     op_obj    i32 [E][cap]   id of Agent::op_obj or -1
 //     meta      u8  [E][cap]   bit0 dead | bits1-2 last_op | bits4-5 group
 //   groups
-//     grp_ids   i32 [E][G][cap] the ordered agent vector of each group (Group::agents)
+//     grp_ids   u16 [E][G][cap] the ordered agent vector of each group (Group::agents)
 //     grp_n, grp_dead i32 [E][G];  grp_reward f32 [E][G]
 //   id_counter i32 [E], rng u32 [E] (minstd_rand0 state, GridWorld.h:106)
 //   pending actions since the last step (GridWorld::set_action, GridWorld.cc:430-496)
@@ -80,10 +80,10 @@ struct State {                      // device pointers; every array is [E][strid
     float* hp;
     float* next_r;
     float* last_r;
-    int32_t* last_act;
+    uint8_t* last_act;
     int32_t* op_obj;
     uint8_t* meta;
-    int32_t* grp_ids;               // [E][G][cap]
+    uint16_t* grp_ids;              // [E][G][cap]
     int32_t* grp_n;                 // [E][G]
     int32_t* grp_dead;              // [E][G]
     float* grp_reward;              // [E][G]
@@ -119,7 +119,10 @@ struct RolloutArgs {
     uint32_t policy_seed;
     uint32_t step_index;            // global step counter (policy RNG stream)
     float eps;                      // random-action probability of the rush policy
-    const int32_t* order;           // [E] queue order of the launch (k_env_order)
+    int32_t* cls_cnt;               // [3][8] envs per weight class: launch L reads [L % 3], appends to
+                                    //   [(L + 1) % 3] and zeroes [(L + 2) % 3]  (L = queue phase)
+    int32_t* cls_list;              // [2][8][cls_stride] env indices per class, read [L % 2], written
+    int cls_stride;                 //   [(L + 1) % 2]
     int32_t* work;                  // [2] env work-queue counters; launch k uses work[k & 1]
     int work_sel;                   //     and zeroes the other one for launch k + 1
     const uint4* reset_image;       // LDS image of the env right after reset + template placement,
