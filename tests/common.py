@@ -10,6 +10,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "mean-field-multi-agent-reinforcement-learning_amd")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 HIP_LIB = os.path.join(PKG, "build", "libmagent.so")
+PY_DIR = os.path.join(PKG, "python")
 ORACLE_LIB = os.path.join(REPO, "oracle", "build", "libbattle_oracle.so")
 REF_LIB = os.path.join(REPO, "oracle", "_ref", "libmagent_ref.so")
 

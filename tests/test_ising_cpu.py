@@ -46,3 +46,19 @@ def test_reference_stream_reproduces_initial_spins_and_first_actions():
     # step 0: Q == 0 -> p = [0.5, 0.5] -> action = (u >= 0.5)
     np.testing.assert_array_equal((u[0] >= 0.5).astype(np.int8), fx["actions"][0])
     assert (mask == 0xFFFFFFFF).all() or c["n_agents"] % 32 != 0
+
+
+def test_dropin_examples_wins_over_a_namespace_examples(tmp_path):
+    """main_MFQ_Ising.py sits next to the reference's namespace package `examples/`; the drop-in's
+    regular `examples` package must still be the one `examples.ising_model` resolves to."""
+    import subprocess
+    import sys
+    shadow = tmp_path / "examples" / "ising_model"
+    shadow.mkdir(parents=True)
+    (shadow / "__init__.py").write_text("raise ImportError('the namespace portion was imported')\n")
+    code = ("import sys; sys.path.insert(0, %r); import examples.ising_model as m; print(m.__file__)"
+            % str(tmp_path))
+    env = dict(os.environ, PYTHONPATH=common.PY_DIR)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().startswith(common.PY_DIR), out.stdout
