@@ -1,0 +1,117 @@
+"""ValueNet (algo/base.py:7-279) on PyTorch-ROCm: eval / target Q networks, greedy act, the MF-Q
+target on device (HIP kernel mfx_mfq_target), masked-MSE Adam step, soft target update.
+
+Inputs may be numpy arrays (the reference's call sites) or device tensors (the batched engine);
+outputs follow the reference: act -> int32 numpy, calc_target_q -> float64, train -> (loss, stats).
+"""
+import copy
+
+import numpy as np
+import torch
+
+from .. import mf
+from .nets import QNet
+
+
+def as_dev(x, dtype=torch.float32):
+    if isinstance(x, torch.Tensor):
+        return x.to(device="cuda", dtype=dtype)
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device="cuda")
+
+
+class ValueNet:
+    def __init__(self, sess, env, handle, name, update_every=5, use_mf=False, learning_rate=1e-4, tau=0.005,
+                 gamma=0.95):
+        self.env = env
+        self.name = name
+        self.name_scope = name or "ValueNet"
+        self.handle = handle
+        self.view_space = tuple(env.get_view_space(handle))
+        assert len(self.view_space) == 3
+        self.feature_space = tuple(env.get_feature_space(handle))
+        self.num_actions = env.get_action_space(handle)[0]
+        self.update_every = update_every
+        self.use_mf = use_mf
+        self.temperature = 0.1
+        self.lr = learning_rate
+        self.tau = tau
+        self.gamma = gamma
+        self.eval_net = QNet(self.view_space, self.feature_space, self.num_actions, use_mf).cuda()
+        self.target_net = copy.deepcopy(self.eval_net)     # TF initialises both; any start works
+        for p in self.target_net.parameters():
+            p.requires_grad_(False)
+        self.optimizer = torch.optim.Adam(self.eval_net.parameters(), lr=self.lr)
+
+    @property
+    def vars(self):
+        """Parameters in a fixed order (eval net, then target net), like the scope's variables."""
+        return list(self.eval_net.parameters()) + list(self.target_net.parameters())
+
+    def _prob(self, kwargs, n):
+        if not self.use_mf:
+            return None
+        assert kwargs.get("prob", None) is not None
+        return as_dev(kwargs["prob"]).reshape(n, self.num_actions)
+
+    def calc_target_q(self, **kwargs):
+        """kwargs: obs, feature, prob (mean field), dones, rewards -> float64 [n] (numpy)."""
+        return self.calc_target_q_dev(**kwargs).cpu().numpy()
+
+    @torch.no_grad()
+    def calc_target_q_dev(self, **kwargs):
+        obs, feat = as_dev(kwargs["obs"]), as_dev(kwargs["feature"])
+        prob = self._prob(kwargs, len(obs))
+        t_q = self.target_net(obs, feat, prob)
+        e_q = self.eval_net(obs, feat, prob)
+        return mf.mfq_target(e_q.float().contiguous(), t_q.float().contiguous(), as_dev(kwargs["rewards"]),
+                             as_dev(kwargs["dones"], torch.uint8), self.gamma)
+
+    @torch.no_grad()
+    def update(self):
+        """Soft update: target = tau * eval + (1 - tau) * target."""
+        for t, e in zip(self.target_net.parameters(), self.eval_net.parameters()):
+            t.mul_(1.0 - self.tau).add_(self.tau * e)
+
+    @torch.no_grad()
+    def act_dev(self, **kwargs):
+        """Device in, device out: int32 actions = argmax softmax(e_q / temperature)."""
+        view, feat = as_dev(kwargs["state"][0]), as_dev(kwargs["state"][1])
+        self.temperature = kwargs["eps"]
+        prob = self._prob(kwargs, len(view))
+        if self.use_mf:
+            assert len(prob) == len(view)
+        e_q = self.eval_net(view, feat, prob)
+        return torch.argmax(torch.softmax(e_q / self.temperature, dim=1), dim=1).to(torch.int32)
+
+    def act(self, **kwargs):
+        return self.act_dev(**kwargs).cpu().numpy().astype(np.int32)
+
+    def train(self, **kwargs):
+        """kwargs: state [obs, feature], target_q, prob, acts, masks -> (loss, {'Eval-Q', 'Target-Q'})."""
+        obs, feat = as_dev(kwargs["state"][0]), as_dev(kwargs["state"][1])
+        prob = self._prob(kwargs, len(obs))
+        target = as_dev(kwargs["target_q"])
+        mask = as_dev(kwargs["masks"])
+        acts = as_dev(kwargs["acts"], torch.int64)
+        e_q = self.eval_net(obs, feat, prob)
+        e_q_max = e_q.gather(1, acts.reshape(-1, 1)).reshape(-1)
+        loss = torch.sum(torch.square(target - e_q_max) * mask) / torch.sum(mask)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        self.optimizer.step()
+        return loss.item(), {"Eval-Q": np.round(e_q_max.mean().item(), 6), "Target-Q": np.round(target.mean().item(), 6)}
+
+    def _save(self, dir_path, prefix, step):
+        import os
+        os.makedirs(dir_path, exist_ok=True)
+        path = os.path.join(dir_path, "{}_{}.pt".format(prefix, step))
+        torch.save({"eval": self.eval_net.state_dict(), "target": self.target_net.state_dict()}, path)
+        print("[*] Model saved at: {}".format(path))
+
+    def _load(self, dir_path, prefix, step):
+        import os
+        path = os.path.join(dir_path, "{}_{}.pt".format(prefix, step))
+        state = torch.load(path, map_location="cuda", weights_only=True)
+        self.eval_net.load_state_dict(state["eval"])
+        self.target_net.load_state_dict(state["target"])
+        print("[*] Loaded model from {}".format(path))
