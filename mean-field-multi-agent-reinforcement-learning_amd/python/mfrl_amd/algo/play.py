@@ -9,6 +9,7 @@
 """
 import math
 import random
+import time
 
 import numpy as np
 import torch
@@ -135,6 +136,8 @@ def play_batched(eng, n_round, map_size, max_steps, models, print_every=50, eps=
     mean_rewards = [[] for _ in range(G)]
     total_rewards = [[] for _ in range(G)]
     step_ct = 0
+    t_play = time.time()
+    agent_steps = 0
     while step_ct < max_steps and not bool(finished.all().item()):
         valid = []
         for g in range(G):
@@ -155,6 +158,7 @@ def play_batched(eng, n_round, map_size, max_steps, models, print_every=50, eps=
             eng.get(g, GET_REWARD, rew_t[g], rowcap)
             eng.get(g, GET_ALIVE, alive_t[g], rowcap)
         sel0 = valid[0].nonzero().reshape(-1)
+        agent_steps += int(valid[0].sum().item()) + int(valid[1].sum().item())
         if train:
             keys = env_of_row[sel0].long() * key_stride + ids_t[0][sel0].long()
             models[0].flush_buffer(state=[view[0].reshape((-1,) + v_shape)[sel0], feat[0].reshape((-1,) + f_shape)[sel0]],
@@ -176,8 +180,14 @@ def play_batched(eng, n_round, map_size, max_steps, models, print_every=50, eps=
         step_ct += 1
         if step_ct % print_every == 0:
             print("> step #{}, Ave-Reward: {}, NUM: {}".format(step_ct, np.round([m[-1] for m in mean_rewards], 6), nums))
+    torch.cuda.synchronize()
+    t_play = time.time() - t_play
+    t_train = time.time()
     if train:
         models[0].train()
+        torch.cuda.synchronize()
+    print("[TIME] play {} steps x {} envs: {:.2f} s ({:.3g} agent-steps/s incl. policy forward); train {:.2f} s"
+          .format(step_ct, E, t_play, agent_steps / max(t_play, 1e-9), time.time() - t_train))
     for g in range(G):
         mean_rewards[g] = sum(mean_rewards[g]) / max(len(mean_rewards[g]), 1)
         total_rewards[g] = sum(total_rewards[g])

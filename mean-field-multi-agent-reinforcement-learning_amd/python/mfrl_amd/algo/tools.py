@@ -53,6 +53,11 @@ class MetaBuffer:
 
     def append(self, value):
         value = _dev(value, self.data.dtype, self.device)
+        if len(value) > self.max_len:             # only the last max_len rows survive in the ring
+            skip = len(value) - self.max_len
+            self._flag = (self._flag + skip) % self.max_len
+            self.length = self.max_len
+            value = value[skip:]
         num, start = len(value), 0
         if self._flag + num > self.max_len:
             tail = self.max_len - self._flag

@@ -9,6 +9,7 @@ Logs go to data/tmp/<algo>.jsonl, models to data/models/<algo>-{0,1}/<algo>_<rou
 """
 import argparse
 import os
+import time
 
 import torch
 
@@ -50,8 +51,11 @@ def main(argv=None):
     handles = env.get_handles()
     log_dir = os.path.join(args.base_dir, "data/tmp")
     model_dir = os.path.join(args.base_dir, "data/models/{}".format(args.algo))
-    models = [spawn_ai(args.algo, None, env, handles[0], args.algo + "-me", args.max_steps),
-              spawn_ai(args.algo, None, env, handles[1], args.algo + "-opponent", args.max_steps)]
+    # the reference's 80000 replay rows are sized for one env; with E envs keep E times as many
+    # (capped at 2M rows = 9.5 GB of views in HBM)
+    memory = min(80000 * args.envs, 2000000)
+    models = [spawn_ai(args.algo, None, env, handles[0], args.algo + "-me", args.max_steps, memory_size=memory),
+              spawn_ai(args.algo, None, env, handles[1], args.algo + "-opponent", args.max_steps, memory_size=memory)]
     play_handle = play
     if args.envs > 1:
         from .battle import BattleBatch
@@ -65,7 +69,10 @@ def main(argv=None):
                           log_name=args.algo, log_dir=log_dir, model_dir=model_dir, train=True)
     for k in range(args.n_round):
         eps = linear_decay(k, [0, int(args.n_round * 0.8), args.n_round], [1, 0.2, 0.1])
+        t0 = time.time()
         runner.run(eps, k)
+        torch.cuda.synchronize()
+        print("[TIME] round {}: {:.2f} s ({} envs)".format(k, time.time() - t0, args.envs))
 
 
 if __name__ == "__main__":

@@ -18,6 +18,10 @@ class Ring:
 
     def append(self, rows):
         rows = np.asarray(rows, dtype=self.data.dtype)
+        if len(rows) > self.max_len:                  # row by row, only the last max_len would remain
+            for k in range(len(rows)):
+                self.append(rows[k:k + 1])
+            return
         n, cut = len(rows), 0
         if self.flag + n > self.max_len:
             cut = self.max_len - self.flag

@@ -35,7 +35,8 @@ def _episode(rng, n_agents, steps, die_p):
     return pushes
 
 
-@pytest.mark.parametrize("use_mean,sub_len,max_len", [(True, 400, 5000), (False, 400, 700), (True, 7, 5000)])
+@pytest.mark.parametrize("use_mean,sub_len,max_len", [(True, 400, 5000), (False, 400, 700), (True, 7, 5000),
+                                                     (True, 400, 300)])
 def test_memory_group_matches_oracle(use_mean, sub_len, max_len):
     rng = np.random.default_rng(3)
     dev = tools.MemoryGroup(V, F, A, max_len, 64, sub_len, use_mean=use_mean, device="cpu")
