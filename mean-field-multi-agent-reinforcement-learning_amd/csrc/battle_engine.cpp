@@ -658,7 +658,95 @@ public:
             return 0;
         }
         if (!strcmp(name, "both_attack")) { ib[0] = 0; return 0; }   // statistics are compiled off (GridWorld.cc:501)
+        if (!strcmp(name, "mean_info")) return mean_info(group, (float*)buf);
         return fail("unsupported info name in get_info: %s", name);
+    }
+
+    // ---- get_info extras (GridWorld.cc:811-954), env 0, from the device state
+    std::vector<int> group_pos(int g) {              // x, y per agent in group order (dead included)
+        const int n = num_env0(g);
+        std::vector<int> pos((size_t)2 * std::max(n, 1));
+        if (n > 0 && host_get(g, kGetPos, pos.data(), 8) != 0) throw HipFailure("get pos");
+        pos.resize((size_t)2 * n);
+        return pos;
+    }
+
+    int mean_info(int group, float* out) {           // GridWorld.cc:832-853
+        const int n = num_env0(group), na = gtype(group).n_action;
+        if (n == 0) return fail("mean_info of an empty group");          // the reference asserts
+        std::vector<int> pos = group_pos(group), act((size_t)n);
+        MFX_CHECK(host_get(group, kGetLastAct, act.data(), 4));
+        float sum_x = 0, sum_y = 0;
+        std::vector<int> counter((size_t)na, 0);
+        for (int i = 0; i < n; i++) {
+            sum_x += (float)pos[2 * i];
+            sum_y += (float)pos[2 * i + 1];
+            if (act[i] >= 0 && act[i] < na) counter[act[i]]++;   // before the first set_action the
+        }                                                         // reference indexes out of range
+        out[0] = sum_x / (float)n;
+        out[1] = sum_y / (float)n;
+        for (int k = 0; k < na; k++) out[2 + k] = (float)(1.0 * counter[k] / n);
+        return 0;
+    }
+
+    // Keys the python wrapper asks with group -1 (gridworld.py:526-636).
+    int get_info_global(int group, const char* name, void* buf) {
+        int* ib = (int*)buf;
+        float* fb = (float*)buf;
+        const int G = n_groups();
+        if (!strcmp(name, "global_minimap")) {       // GridWorld.cc:807-830
+            const int vh = (int)lround(fb[0]), vw = (int)lround(fb[1]);
+            if (vh <= 0 || vw <= 0) return fail("global_minimap: bad size %d x %d", vh, vw);
+            memset(fb, 0, sizeof(float) * vh * vw * G);
+            const int sh = (H + vh - 1) / vh, sw = (W + vw - 1) / vw;
+            for (int i = 0; i < G; i++) {
+                // the reference computes (i - group + n_group) % n_group in size_t; group -1 -> (i+1) % n
+                const size_t ch = ((size_t)i - (size_t)(long)group + (size_t)G) % (size_t)G;
+                std::vector<int> pos = allocated ? group_pos(i) : std::vector<int>();
+                const size_t n = pos.size() / 2;
+                for (size_t j = 0; j < n; j++) fb[((size_t)(pos[2 * j + 1] / sh) * vw + pos[2 * j] / sw) * G + ch] += 1.0f;
+                for (int y = 0; y < vh; y++)
+                    for (int x = 0; x < vw; x++) fb[((size_t)y * vw + x) * G + ch] /= (float)n;
+            }
+            return 0;
+        }
+        if (!strcmp(name, "walls_info")) {           // GridWorld.cc:854-863, Map.cc:621-627 (scan order)
+            std::vector<uint16_t> cells((size_t)W * H);
+            if (allocated) MFX_HIP(hipMemcpy(cells.data(), s.cells, cells.size() * 2, hipMemcpyDeviceToHost));
+            int n = 0;
+            for (int c = 0; c < W * H; c++)
+                if (allocated && cells[c] == kCellWall) { ++n; ib[2 * n] = c % W; ib[2 * n + 1] = c / W; }
+            ib[0] = n;
+            return 0;
+        }
+        if (!strcmp(name, "render_window_info")) {   // GridWorld.cc:864-896 (no attack events: no renderer)
+            const int x1 = ib[0], y1 = ib[1], x2 = ib[2], y2 = ib[3];
+            int ct = 1;
+            for (int i = 0; i < G; i++) {
+                std::vector<int> pos = allocated ? group_pos(i) : std::vector<int>();
+                std::vector<int> ids(pos.size() / 2);
+                if (!ids.empty()) MFX_CHECK(host_get(i, kGetId, ids.data(), 4));
+                for (size_t j = 0; j < ids.size(); j++) {
+                    const int x = pos[2 * j], y = pos[2 * j + 1];
+                    if (x < x1 || x > x2 || y < y1 || y > y2) continue;
+                    ib[4 * ct] = ids[j]; ib[4 * ct + 1] = x; ib[4 * ct + 2] = y; ib[4 * ct + 3] = i;
+                    ct++;
+                }
+            }
+            ib[0] = ct - 1;
+            ib[1] = 0;
+            return 0;
+        }
+        if (!strcmp(name, "attack_event")) return 0;  // recorded by the renderer only: none
+        if (!strcmp(name, "groups_info")) {          // GridWorld.cc:934-949
+            static const int colors[4][3] = {{192, 64, 64}, {64, 64, 192}, {64, 192, 64}, {64, 64, 64}};
+            for (int i = 0; i < G; i++) {
+                ib[5 * i] = 1; ib[5 * i + 1] = 1;     // 1 x 1 bodies (width, length)
+                for (int k = 0; k < 3; k++) ib[5 * i + 2 + k] = colors[i][k];
+            }
+            return 0;
+        }
+        return get_info(group, name, buf);
     }
 };
 
@@ -692,7 +780,7 @@ MFX_API int env_get_reward(void* game, int group, float* buffer) {
     MFX_GUARD(MFX_ENV(game)->host_get(group, mfx::kGetReward, buffer, 4));
 }
 MFX_API int env_get_info(void* game, int group, const char* name, void* buffer) {
-    MFX_GUARD(MFX_ENV(game)->get_info(group, name, buffer));
+    MFX_GUARD(MFX_ENV(game)->get_info_global(group, name, buffer));
 }
 MFX_API int env_render(void* game) { (void)game; return 0; }              // visualization: out of scope
 MFX_API int env_render_next_file(void* game) { (void)game; return 0; }

@@ -1234,6 +1234,7 @@ __global__ void __launch_bounds__(256) k_get(const GameParams* __restrict__ gp, 
                 reinterpret_cast<int*>(out)[2 * (o + i) + 1] = (int)(p >> 16);
             } break;
             case kGetHp: reinterpret_cast<float*>(out)[o + i] = v.hp[id]; break;
+            case kGetLastAct: reinterpret_cast<int*>(out)[o + i] = v.last_act[id]; break;
             default: break;
         }
     }

@@ -210,6 +210,43 @@ class GridWorld(Environment):
     def set_seed(self, seed):
         self._lib.env_config_game(self.game, b"seed", ctypes.byref(ctypes.c_int(seed)))
 
+    # ------------------------------------------------------------------ get_info extras (gridworld.py:486-636)
+    def _call_info(self, group, name, buf):
+        self._lib.env_get_info(self.game, group, name, buf.ctypes.data_as(ctypes.c_void_p))   # checked
+        return buf
+
+    def get_mean_info(self, handle):
+        """float32 [2 + n_action]: mean x, mean y, action frequencies (deprecated in the reference)."""
+        buf = np.empty(2 + self.get_action_space(handle)[0], dtype=np.float32)
+        return self._call_info(_hv(handle), b"mean_info", buf)
+
+    def get_global_minimap(self, height, width):
+        """float32 [height, width, n_group]: per-group agent density over a downsampled map."""
+        buf = np.empty((height, width, len(self.group_handles)), dtype=np.float32)
+        buf[0, 0, 0] = height
+        buf[0, 0, 1] = width
+        return self._call_info(-1, b"global_minimap", buf)
+
+    def _get_groups_info(self):
+        buf = np.empty((len(self.group_handles), 5), dtype=np.int32)
+        return self._call_info(-1, b"groups_info", buf)
+
+    def _get_walls_info(self):
+        buf = np.empty((100 * 100, 2), dtype=np.int32)
+        self._call_info(-1, b"walls_info", buf)
+        return buf[1:1 + buf[0, 0]]
+
+    def _get_render_info(self, x_range, y_range):
+        n = sum(self.get_num(h) for h in self.group_handles)
+        buf = np.empty((n + 1, 4), dtype=np.int32)
+        buf[0] = x_range[0], y_range[0], x_range[1], y_range[1]
+        self._call_info(-1, b"render_window_info", buf)
+        agent_ct, attack_event_ct = buf[0, 0], buf[0, 1]
+        agent_info = {int(item[0]): [int(item[1]), int(item[2]), int(item[3])] for item in buf[1:1 + agent_ct]}
+        events = np.empty((attack_event_ct, 3), dtype=np.int32)
+        self._call_info(-1, b"attack_event", events)
+        return agent_info, events
+
     # ------------------------------------------------------------------ render (out of scope: no-op)
     def set_render_dir(self, name):
         if not os.path.exists(name):

@@ -86,3 +86,42 @@ def test_hip_matches_oracle_random_scenarios(map_size, n0, n1, seed, walls):
     assert len(got) == len(ref)
     first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
     assert first_bad is None, "first divergence at step %s" % first_bad
+
+
+def test_get_info_extras_match_reference():
+    """get_info extras: global_minimap, mean_info, walls_info,
+    render_window_info, groups_info -- HIP engine against the reference build (oracle/_ref) on the
+    same scenario (custom walls, a few steps, dead agents still listed before clear_dead)."""
+    if not os.path.exists(common.REF_LIB):
+        pytest.skip("reference build absent")
+    import magent
+    outs = {}
+    for name, path in (("hip", common.HIP_LIB), ("ref", common.REF_LIB)):
+        env, h = common.battle_env(path, 30)
+        env.reset()
+        env.add_agents(-1, method="custom", pos=[[5, 5], [5, 6], [6, 6], [20, 3]])
+        left, right = bd.block_positions(30, 18)
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        rs = np.random.RandomState(4)
+        for t in range(6):
+            for g in range(2):
+                env.get_observation(h[g])
+                env.set_action(h[g], rs.randint(0, 21, env.get_num(h[g])).astype(np.int32))
+            env.step()
+            if t < 5:
+                env.clear_dead()
+        o = {"minimap": env.get_global_minimap(7, 9).copy(), "minimap13": env.get_global_minimap(13, 13).copy(),
+             "walls": env._get_walls_info().copy(), "groups": env._get_groups_info().copy()}
+        for g in range(2):
+            o["mean%d" % g] = env.get_mean_info(h[g]).copy()
+        ai, ev = env._get_render_info((3, 25), (2, 20))
+        o["render"] = sorted(ai.items())
+        o["events"] = ev.shape[0]
+        outs[name] = o
+    for k in outs["ref"]:
+        a, b = outs["hip"][k], outs["ref"][k]
+        if isinstance(b, np.ndarray):
+            assert a.tobytes() == b.tobytes(), k
+        else:
+            assert a == b, k
