@@ -10,7 +10,10 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <map>
 #include <memory>
 #include <string>
@@ -118,6 +121,10 @@ public:
     uint32_t* d_sort = nullptr;
     int32_t* d_err = nullptr;
     bool allocated = false;
+    // render (RenderGenerator.cc): config.json + video_<file>.txt frames of env 0
+    std::string render_dir;
+    int file_ct = 0, frame_ct = 0, frame_per_file = 10000;
+    bool first_render = true;
     int max_ids = 0;                                 // upper bound of id_counter over envs
     std::vector<int> group_ub;                       // upper bound of grp_n per group
     int pending_ub = 0;                              // upper bound of queued actions
@@ -171,7 +178,7 @@ public:
         else if (!strcmp(key, "minimap_mode")) minimap = *(bool*)p;
         else if (!strcmp(key, "goal_mode")) goal = *(bool*)p;
         else if (!strcmp(key, "embedding_size")) emb = *(int*)p;
-        else if (!strcmp(key, "render_dir")) { /* rendering is out of scope */ }
+        else if (!strcmp(key, "render_dir")) render_dir = (const char*)p;
         else if (!strcmp(key, "seed")) {
             const unsigned long sv = (unsigned long)(long)*(int*)p;
             const uint64_t x = sv % 2147483647UL;
@@ -301,6 +308,7 @@ public:
                 RP.val[k] = R.val[k];
             }
         }
+        p.record_events = first_render ? 0 : 1;
         p.par_step = 1;
         for (int g = 0; g < p.n_groups; g++) p.par_step &= p.type[g].kill_supply == 0.0f;
         gp = p;
@@ -340,6 +348,9 @@ public:
             while (na < need_actions) na *= 2;
             const int oa = s.acap;
             grow(s.atk, E, oa, na); grow(s.mov, E, oa, na); grow(d_sort, E, oa, na);
+            if (s.ev) (void)hipFree(s.ev);
+            alloc(s.ev, 1 + (size_t)3 * na);
+            MFX_HIP_THROW(hipMemset(s.ev, 0, sizeof(int32_t)));
             s.acap = na;
         }
     }
@@ -369,6 +380,7 @@ public:
             }
             MFX_HIP_THROW(hipMemcpyAsync(d_gp, &gp, sizeof(GameParams), hipMemcpyHostToDevice, stream));
             MFX_HIP_THROW(launch_reset(d_gp, s, stream));
+            next_file();                              // GridWorld.cc:102
             max_ids = 0;
             std::fill(group_ub.begin(), group_ub.end(), 0);
             pending_ub = 0;
@@ -662,6 +674,118 @@ public:
         return fail("unsupported info name in get_info: %s", name);
     }
 
+    // ---- rendering (GridWorld.cc:1023-1033, RenderGenerator.cc): frames of env 0
+    void next_file() { file_ct++; frame_ct = 0; }
+
+    void start_recording() {                      // events are kept once first_render is false
+        if (!first_render) return;
+        first_render = false;
+        gp.record_events = 1;
+        if (allocated) MFX_HIP_THROW(hipMemcpy(d_gp, &gp, sizeof(GameParams), hipMemcpyHostToDevice));
+    }
+
+    std::vector<int> attack_events() {            // (id, x, y) triples of the last step
+        std::vector<int> ev;
+        if (first_render || !allocated) return ev;
+        MFX_HIP_THROW(hipStreamSynchronize(stream));
+        int n = 0;
+        MFX_HIP_THROW(hipMemcpy(&n, s.ev, sizeof(int), hipMemcpyDeviceToHost));
+        ev.resize((size_t)3 * n);
+        if (n) MFX_HIP_THROW(hipMemcpy(ev.data(), s.ev + 1, sizeof(int) * ev.size(), hipMemcpyDeviceToHost));
+        return ev;
+    }
+
+    static std::string rgba(int r, int g, int b, float alpha) {
+        std::stringstream ss;
+        ss << "\"rgba(" << r << "," << g << "," << b << "," << alpha << ")\"";
+        return ss.str();
+    }
+
+    template <class T> static void json(std::ofstream& os, const char* key, T value, bool last = false) {
+        os << "\"" << key << "\": " << value;
+        os << (last ? "" : ",") << std::endl;
+    }
+
+    void gen_config() {                           // RenderGenerator.cc:58-111
+        static const int colors[4][3] = {{192, 64, 64}, {64, 64, 192}, {64, 192, 64}, {64, 64, 64}};
+        std::ofstream f(render_dir + "/" + "config.json");
+        f << "{" << std::endl;
+        json(f, "width", W);
+        json(f, "height", H);
+        json(f, "static-file", "\"static.map\"");
+        json(f, "obstacle-style", rgba(127, 127, 127, 1));
+        json(f, "dynamic-file-directory", "\".\"");
+        json(f, "attack-style", rgba(63, 63, 63, 0.8f));
+        json(f, "minimap-width", 300);
+        json(f, "minimap-height", 250);
+        f << "\"group\" : [" << std::endl;
+        const int G = n_groups();
+        for (int i = 0; i < G; i++) {
+            const AgentTypeSpec& t = gtype(i);
+            const int* c = colors[i];
+            f << "{" << std::endl;
+            json(f, "height", t.length);
+            json(f, "width", t.width);
+            json(f, "style", rgba(c[0], c[1], c[2], 1));
+            json(f, "anchor", "[0, 0]");
+            json(f, "max-speed", (int)t.speed);
+            json(f, "speed-style", rgba(c[0], c[1], c[2], 0.01f));
+            json(f, "vision-radius", t.view_radius);
+            json(f, "vision-angle", t.view_angle);
+            json(f, "vision-style", rgba(c[0], c[1], c[2], 0.2f));
+            json(f, "attack-radius", t.attack_radius);
+            json(f, "attack-angle", t.attack_angle);
+            json(f, "attack-style", rgba(c[0], c[1], c[2], 0.1f));
+            json(f, "broadcast-radius", 1, true);
+            f << (i == G - 1 ? "}" : "},") << std::endl;
+        }
+        f << "]" << std::endl;
+        f << "}" << std::endl;
+    }
+
+    int render() {                                // GridWorld::render + RenderGenerator::render_a_frame
+        if (render_dir.empty()) return 0;
+        if (render_dir == "___debug___") return 0;   // the reference prints the map to stdout
+        try {
+            if (first_render) { start_recording(); gen_config(); }
+            const int G = n_groups();
+            std::ofstream fout(render_dir + "/" + "video_" + std::to_string(file_ct) + ".txt",
+                               frame_ct == 0 ? std::ios::out : std::ios::app);
+            if (frame_ct == 0) {
+                std::vector<int> walls(2 * (size_t)W * H + 2);
+                get_info_global(-1, "walls_info", walls.data());
+                fout << "W" << " " << walls[0] << std::endl;
+                for (int i = 1; i <= walls[0]; i++) fout << walls[2 * i] << " " << walls[2 * i + 1] << std::endl;
+            }
+            std::vector<int> ev = attack_events();
+            int num_agents = 0;
+            for (int i = 0; i < G; i++) num_agents += allocated ? num_env0(i) : 0;
+            fout << "F" << " " << num_agents << " " << (int)(ev.size() / 3) << " " << 0 << std::endl;
+            for (int i = 0; i < G && allocated; i++) {
+                const int n = num_env0(i);
+                if (!n) continue;
+                std::vector<int> ids(n), pos(2 * (size_t)n);
+                std::vector<float> hp(n);
+                MFX_CHECK(host_get(i, kGetId, ids.data(), 4));
+                MFX_CHECK(host_get(i, kGetPos, pos.data(), 8));
+                MFX_CHECK(host_get(i, kGetHp, hp.data(), 4));
+                const float max_hp = gtype(i).hp;
+                for (int j = 0; j < n; j++) {
+                    int h = std::max(0, int(100 * hp[j] / max_hp));
+                    h = std::min(h, 100);
+                    fout << ids[j] << " " << h << " " << 270 << " " << pos[2 * j] << " " << pos[2 * j + 1] << " " << i
+                         << std::endl;                    // dir2angle[NORTH] = 270 (turn mode off)
+                }
+            }
+            for (size_t k = 0; k < ev.size(); k += 3)
+                fout << 0 << " " << ev[k] << " " << ev[k + 1] << " " << ev[k + 2] << std::endl;
+            if (frame_ct++ > frame_per_file) { frame_ct = 0; file_ct++; }
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        return 0;
+    }
+
     // ---- get_info extras (GridWorld.cc:811-954), env 0, from the device state
     std::vector<int> group_pos(int g) {              // x, y per agent in group order (dead included)
         const int n = num_env0(g);
@@ -719,7 +843,7 @@ public:
             ib[0] = n;
             return 0;
         }
-        if (!strcmp(name, "render_window_info")) {   // GridWorld.cc:864-896 (no attack events: no renderer)
+        if (!strcmp(name, "render_window_info")) {   // GridWorld.cc:864-896
             const int x1 = ib[0], y1 = ib[1], x2 = ib[2], y2 = ib[3];
             int ct = 1;
             for (int i = 0; i < G; i++) {
@@ -734,10 +858,15 @@ public:
                 }
             }
             ib[0] = ct - 1;
-            ib[1] = 0;
+            ib[1] = (int)(attack_events().size() / 3);
+            start_recording();                        // GridWorld.cc:882
             return 0;
         }
-        if (!strcmp(name, "attack_event")) return 0;  // recorded by the renderer only: none
+        if (!strcmp(name, "attack_event")) {         // GridWorld.cc:919-926
+            std::vector<int> ev = attack_events();
+            std::copy(ev.begin(), ev.end(), ib);
+            return 0;
+        }
         if (!strcmp(name, "groups_info")) {          // GridWorld.cc:934-949
             static const int colors[4][3] = {{192, 64, 64}, {64, 64, 192}, {64, 192, 64}, {64, 64, 64}};
             for (int i = 0; i < G; i++) {
@@ -782,8 +911,8 @@ MFX_API int env_get_reward(void* game, int group, float* buffer) {
 MFX_API int env_get_info(void* game, int group, const char* name, void* buffer) {
     MFX_GUARD(MFX_ENV(game)->get_info_global(group, name, buffer));
 }
-MFX_API int env_render(void* game) { (void)game; return 0; }              // visualization: out of scope
-MFX_API int env_render_next_file(void* game) { (void)game; return 0; }
+MFX_API int env_render(void* game) { MFX_GUARD(MFX_ENV(game)->render()); }
+MFX_API int env_render_next_file(void* game) { MFX_GUARD((MFX_ENV(game)->next_file(), 0)); }
 
 MFX_API int gridworld_register_agent_type(void* game, const char* name, int n, const char** keys, float* values) {
     MFX_GUARD(MFX_ENV(game)->register_type(name, n, keys, values));

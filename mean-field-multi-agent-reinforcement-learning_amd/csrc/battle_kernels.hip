@@ -675,8 +675,9 @@ __device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem
     }
 }
 
+// ev (render, GridWorld.cc:531-535): every live attacker's (id, target x, target y), blank or not.
 __device__ __forceinline__ void do_attack_serial(const GameParams& gp, const StepSmem& sm, EnvView& v, uint32_t* atk,
-                                                 int n_atk) {
+                                                 int n_atk, int32_t* ev) {
     // shuffled order, strictly sequential (the reference loop is racy with OMP>1; OMP=1 semantics)
     const int W = gp.W, H = gp.H;
     for (int i = 0; i < n_atk; ++i) {
@@ -689,6 +690,11 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, const Ste
         const uint32_t p = v.xy[id];
         const int ox = (int)(p & 0xFFFF) + T.att_x_off + T.att_dx[ai];
         const int oy = (int)(p >> 16) + T.att_y_off + T.att_dy[ai];
+        if (ev) {
+            const int k = ev[0];
+            ev[1 + 3 * k] = id; ev[2 + 3 * k] = ox; ev[3 + 3 * k] = oy;
+            ev[0] = k + 1;
+        }
         uint32_t cv = kCellEmpty;
         if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
         if (cv >= kCellWall) { v.next_r[id] += T.attack_penalty; continue; }       // blank
@@ -987,12 +993,13 @@ __device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView&
 template <bool kW>
 __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
                               uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
-                              int& done_out, const bool have_ps, const ParScratch ps, int nid) {
+                              int& done_out, const bool have_ps, const ParScratch ps, int nid,
+                              int32_t* ev = nullptr) {
     const int G = gp.n_groups;
 #ifndef MFX_PAR_MASK
 #define MFX_PAR_MASK 3
 #endif
-    const bool par0 = have_ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x;
+    const bool par0 = !ev && have_ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x;
     bool par = par0 && (MFX_PAR_MASK & 1);
     psync<kW>();
     // ---- shuffle + attack (GridWorld.cc:507-558)
@@ -1014,7 +1021,8 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
             const uint32_t t = atk[i]; atk[i] = atk[j]; atk[j] = t;
         }
         rng = x;
-        do_attack_serial(gp, sm, v, atk, n_atk);
+        if (ev) ev[0] = 0;
+        do_attack_serial(gp, sm, v, atk, n_atk, ev);
     }
     psync<kW>();
     // ---- starve (GridWorld.cc:570-595): independent per agent
@@ -1155,7 +1163,8 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     uint32_t rng = s.rng[e];
     int done = 0;
     load_serial_types(gp, sm);
-    step_env_core<false>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, false, ParScratch{}, nid);
+    int32_t* ev = (gp.record_events && e == 0) ? s.ev : nullptr;
+    step_env_core<false>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, false, ParScratch{}, nid, ev);
     if (lds) {
         for (int i = TID; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
         for (int i = TID; i < nid; i += blockDim.x) {

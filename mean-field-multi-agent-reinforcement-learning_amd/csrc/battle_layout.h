@@ -66,6 +66,7 @@ struct GameParams {
     int W, H, n_groups, minimap, emb, n_ch;
     int large_map, n_sep, band_w;
     int n_rules;
+    int record_events;              // 1 once rendering started: k_step records env 0's attack events
     int par_step;                   // 1: attack / move resolution may run in parallel (every
                                     //    kill_supply == 0, so a kill never changes the killer's hp)
     int feat_size[kMaxGroups];
@@ -95,6 +96,8 @@ struct State {                      // device pointers; every array is [E][strid
     int32_t* n_mov;                 // [E]
     int32_t* done;                  // [E]
     int32_t* err;                   // [1] sticky device-side error code
+    int32_t* ev;                    // [1 + 3 * acap] env 0's attack events of the last step (render):
+                                    //   count, then (attacker id, target x, target y) in shuffle order
 };
 
 // Arguments of the fused rollout step (k_rollout): one launch = one step of the

@@ -20,8 +20,18 @@ def manifest():
         return json.load(f)
 
 
+def pin_ref_threads():
+    """The reference engine's attack loop is an OpenMP loop whose results (kill credit, render
+    event order) depend on the thread count; OMP_NUM_THREADS is only read when libgomp first
+    loads, which may predate conftest (the box exports 16). Set the ICV directly instead."""
+    import ctypes
+    ctypes.CDLL("libgomp.so.1").omp_set_num_threads(1)
+
+
 def battle_env(lib_path, map_size):
     import magent
+    if os.path.abspath(lib_path) == os.path.abspath(REF_LIB):
+        pin_ref_threads()
     lib = magent.load_library(lib_path)
     env = magent.GridWorld("battle", map_size=map_size, lib=lib)
     return env, env.get_handles()

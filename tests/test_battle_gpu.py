@@ -125,3 +125,41 @@ def test_get_info_extras_match_reference():
             assert a.tobytes() == b.tobytes(), k
         else:
             assert a == b, k
+
+
+def test_render_frames_match_reference(tmp_path):
+    """The render frame writer (RenderGenerator.cc): config.json and the
+    video_<n>.txt frames (walls, agents with hp %, attack events in shuffle order) byte for byte
+    against the reference build, over two episodes (a reset starts a new file)."""
+    if not os.path.exists(common.REF_LIB):
+        pytest.skip("reference build absent")
+    counts = {}
+    for name, path in (("hip", common.HIP_LIB), ("ref", common.REF_LIB)):
+        d = tmp_path / name
+        env, h = common.battle_env(path, 26)
+        env.set_render_dir(str(d))
+        rs = np.random.RandomState(11)
+        counts[name] = []
+        for ep in range(2):
+            env.reset()
+            env.add_agents(-1, method="custom", pos=[[4, 4], [4, 5]])
+            left, right = bd.block_positions(26, 18)
+            env.add_agents(h[0], method="custom", pos=left)
+            env.add_agents(h[1], method="custom", pos=right)
+            env.render()
+            for t in range(7):
+                for g in range(2):
+                    env.get_observation(h[g])
+                    env.set_action(h[g], rs.randint(0, 21, env.get_num(h[g])).astype(np.int32))
+                env.step()
+                env.render()
+                _, ev = env._get_render_info((0, 25), (0, 25))
+                counts[name].append(ev.tolist())
+                env.clear_dead()
+    files = sorted(p.name for p in (tmp_path / "ref").iterdir())
+    assert files == sorted(p.name for p in (tmp_path / "hip").iterdir())
+    assert "config.json" in files and len(files) >= 3
+    for f in files:
+        assert (tmp_path / "hip" / f).read_bytes() == (tmp_path / "ref" / f).read_bytes(), f
+    assert counts["hip"] == counts["ref"]
+    assert any(len(c) for c in counts["ref"])
