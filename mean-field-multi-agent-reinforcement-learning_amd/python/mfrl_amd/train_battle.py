@@ -48,6 +48,7 @@ def main(argv=None):
     args = parser.parse_args(argv)
 
     env = magent.GridWorld("battle", map_size=args.map_size)
+    env.set_render_dir(os.path.join(args.base_dir, "examples/battle_model", "build/render"))  # train_battle.py:87
     handles = env.get_handles()
     log_dir = os.path.join(args.base_dir, "data/tmp")
     model_dir = os.path.join(args.base_dir, "data/models/{}".format(args.algo))
