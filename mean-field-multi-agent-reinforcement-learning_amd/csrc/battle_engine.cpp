@@ -16,6 +16,7 @@
 #include <sstream>
 #include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -153,7 +154,7 @@ public:
         for (void* p : {(void*)s.cells, (void*)s.xy, (void*)s.hp, (void*)s.next_r, (void*)s.last_r,
                         (void*)s.last_act, (void*)s.op_obj, (void*)s.meta, (void*)s.grp_ids, (void*)s.grp_n,
                         (void*)s.grp_dead, (void*)s.grp_reward, (void*)s.id_counter, (void*)s.rng, (void*)s.atk,
-                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)d_sort, (void*)d_gp,
+                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)s.idx_mark, (void*)d_sort, (void*)d_gp,
                         (void*)d_err})
             if (p) (void)hipFree(p);
         s = State{}; d_sort = nullptr; d_gp = nullptr; d_err = nullptr; allocated = false;
@@ -249,6 +250,169 @@ public:
         return 0;
     }
 
+    // ------------------------------------------------------------------ reward DSL
+    // The common rule form handled by RuleParams (k_step / k_rollout without the interpreter).
+    bool simple_rule(const Rule& R) const {
+        if (R.on < 0 || R.on >= (int)nodes.size()) return false;
+        const Node& N = nodes[R.on];
+        if (N.op != kEvAttack && N.op != kEvKill && N.op != kEvCollide) return false;
+        if (N.raw.size() < 2) return false;
+        const int sa = N.raw[0], sb = N.raw[1];
+        if (sa < 0 || sb < 0 || sa >= (int)syms.size() || sb >= (int)syms.size()) return false;
+        if (syms[sa].index != -1 || syms[sb].index != -1 || syms[sa].group == syms[sb].group) return false;
+        if ((int)R.recv.size() > kMaxRecv) return false;
+        for (int x : R.recv)
+            if (x != sa && x != sb) return false;
+        return true;
+    }
+
+    // related_symbols / infer_map of a node (GridWorld::collect_related_symbol, RewardEngine.cc:68-101):
+    // std::set / std::map keyed by AgentSymbol*, i.e. ordered by symbol number; map insertion keeps
+    // the first entry for a key.
+    int node_symbols(int ni, std::set<int>& rel, std::map<int, int>& infer, int depth) const {
+        if (ni < 0 || ni >= (int)nodes.size() || depth > kMaxNodes)
+            return fail("reward DSL: bad event node %d", ni);
+        const Node& N = nodes[ni];
+        const auto need = [&](size_t k) { return N.raw.size() >= k; };
+        switch (N.op) {
+            case kEvAnd: case kEvOr: {
+                if (!need(2)) return fail("reward DSL: malformed node %d", ni);
+                std::set<int> r0, r1; std::map<int, int> m0, m1;
+                MFX_CHECK(node_symbols(N.raw[0], r0, m0, depth + 1));
+                MFX_CHECK(node_symbols(N.raw[1], r1, m1, depth + 1));
+                rel.insert(r0.begin(), r0.end()); rel.insert(r1.begin(), r1.end());
+                infer.insert(m0.begin(), m0.end()); infer.insert(m1.begin(), m1.end());
+                return 0;
+            }
+            case kEvNot: {
+                if (!need(1)) return fail("reward DSL: malformed node %d", ni);
+                std::set<int> r0; std::map<int, int> m0;
+                MFX_CHECK(node_symbols(N.raw[0], r0, m0, depth + 1));
+                rel.insert(r0.begin(), r0.end()); infer.insert(m0.begin(), m0.end());
+                return 0;
+            }
+            case kEvKill: case kEvCollide: case kEvAttack:
+                if (!need(2)) return fail("reward DSL: malformed node %d", ni);
+                rel.insert(N.raw[0]); rel.insert(N.raw[1]);
+                infer.insert(std::make_pair(N.raw[0], N.raw[1]));
+                return 0;
+            case kEvAt: case kEvIn: case kEvDie: case kEvInALine:
+                if (!need(N.op == kEvAt ? 3 : N.op == kEvIn ? 5 : 1)) return fail("reward DSL: malformed node %d", ni);
+                rel.insert(N.raw[0]);
+                return 0;
+            case kEvAlign:
+                // reads counter_x / counter_y, which the reference allocates and never fills
+                // (GridWorld.cc:99-100, :1039-1050 commented out): no defined result to reproduce
+                return fail("reward DSL: 'align' reads uninitialised engine memory in the reference; not supported");
+            default:
+                return fail("reward DSL: invalid event op %d", N.op);
+        }
+    }
+
+    int post_order(int ni, std::vector<int>& out, int depth) const {
+        if (depth > kMaxNodes) return fail("reward DSL: event graph too deep");
+        if (std::find(out.begin(), out.end(), ni) != out.end()) return 0;
+        const Node& N = nodes[ni];
+        if (N.op == kEvAnd || N.op == kEvOr) {
+            MFX_CHECK(post_order(N.raw[0], out, depth + 1));
+            MFX_CHECK(post_order(N.raw[1], out, depth + 1));
+        } else if (N.op == kEvNot) {
+            MFX_CHECK(post_order(N.raw[0], out, depth + 1));
+        }
+        out.push_back(ni);
+        return 0;
+    }
+
+    // GridWorld::init_reward_description (RewardEngine.cc:105-208) into a DslProgram.
+    int compile_dsl(DslProgram& P) const {
+        P = DslProgram{};
+        if ((int)syms.size() > kMaxSyms) return fail("reward DSL: at most %d agent symbols", kMaxSyms);
+        if ((int)nodes.size() > kMaxNodes) return fail("reward DSL: at most %d event nodes", kMaxNodes);
+        const int G = n_groups();
+        for (size_t i = 0; i < syms.size(); i++) {
+            if (syms[i].group < 0 || syms[i].group >= G) return fail("reward DSL: symbol %zu has no valid group", i);
+            if (syms[i].index < -2) return fail("reward DSL: symbol %zu has a bad index", i);
+            P.sym[i] = DslSym{syms[i].group, syms[i].index};
+        }
+        auto sym_ok = [&](int x) { return x >= 0 && x < (int)syms.size(); };
+        for (size_t i = 0; i < nodes.size(); i++) {
+            const Node& N = nodes[i];
+            DslNode& D = P.node[i];
+            D = DslNode{N.op, -1, -1, 0, 0, 0, 0};
+            const auto raw = [&](size_t k) { return k < N.raw.size() ? N.raw[k] : -1; };
+            D.a = raw(0); D.b = raw(1);
+            switch (N.op) {
+                case kEvAnd: case kEvOr: case kEvNot:
+                    if (D.a < 0 || D.a >= (int)nodes.size() || (N.op != kEvNot && (D.b < 0 || D.b >= (int)nodes.size())))
+                        return fail("reward DSL: node %zu has a bad input", i);
+                    break;
+                case kEvKill: case kEvCollide: case kEvAttack:
+                    if (!sym_ok(D.a) || !sym_ok(D.b)) return fail("reward DSL: node %zu has a bad symbol", i);
+                    if (syms[D.b].index == -2)       // assert(!symbol_input[1]->is_all()) (RewardEngine.cc:221)
+                        return fail("reward DSL: the object of attack/kill/collide cannot be a whole group");
+                    break;
+                case kEvAt:
+                    if (!sym_ok(D.a)) return fail("reward DSL: node %zu has a bad symbol", i);
+                    D.i0 = raw(1); D.i1 = raw(2);
+                    break;
+                case kEvIn:
+                    if (!sym_ok(D.a)) return fail("reward DSL: node %zu has a bad symbol", i);
+                    D.i0 = raw(1); D.i1 = raw(2); D.i2 = raw(3); D.i3 = raw(4);
+                    break;
+                case kEvDie:
+                    if (!sym_ok(D.a)) return fail("reward DSL: node %zu has a bad symbol", i);
+                    break;
+                case kEvInALine:
+                    if (!sym_ok(D.a) || syms[D.a].index != -2)      // assert(is_all()) (RewardEngine.cc:260)
+                        return fail("reward DSL: in_a_line needs a whole-group symbol");
+                    break;
+                default:
+                    break;                     // reported by node_symbols when a rule uses it
+            }
+        }
+        P.n_rules = (int)rules.size();
+        for (size_t r = 0; r < rules.size(); r++) {
+            const Rule& R = rules[r];
+            DslRule& D = P.rule[r];
+            std::set<int> rel;
+            std::map<int, int> infer;
+            MFX_CHECK(node_symbols(R.on, rel, infer, 0));
+            // input symbols: first the inferable subjects with their objects, then the rest
+            std::vector<int> in, inf;
+            std::set<int> added;
+            for (int x : rel) {
+                if (added.count(x)) continue;
+                auto it = infer.find(x);
+                if (it != infer.end()) {
+                    in.push_back(x); inf.push_back(it->second);
+                    added.insert(x); added.insert(it->second);
+                }
+            }
+            for (int x : rel)
+                if (!added.count(x)) { in.push_back(x); inf.push_back(-1); }
+            if ((int)in.size() > kMaxSyms) return fail("reward rule %zu: too many symbols", r);
+            D.n_in = (int)in.size();
+            for (size_t k = 0; k < in.size(); k++) { D.in_sym[k] = (int8_t)in[k]; D.infer[k] = (int8_t)inf[k]; }
+            std::vector<int> post;
+            MFX_CHECK(post_order(R.on, post, 0));
+            D.n_post = (int)post.size();
+            for (size_t k = 0; k < post.size(); k++) D.post[k] = (int8_t)post[k];
+            if ((int)R.recv.size() > kMaxRecv) return fail("reward rule %zu: too many receivers", r);
+            D.n_recv = (int)R.recv.size();
+            D.terminal = R.terminal;
+            for (size_t k = 0; k < R.recv.size(); k++) {
+                const int x = R.recv[k];
+                if (!sym_ok(x)) return fail("reward rule %zu: bad receiver", r);
+                // a receiver is bound only if the event involves it (RewardEngine.cc:191-193)
+                if (syms[x].index != -2 && !rel.count(x))
+                    return fail("reward rule %zu: receiver %d is not involved in the triggering event", r, x);
+                D.recv[k] = (int8_t)x;
+                D.val[k] = R.val[k];
+            }
+        }
+        return 0;
+    }
+
     // ------------------------------------------------------------------ compile
     int build_params() {
         const int G = n_groups();
@@ -276,37 +440,33 @@ public:
             for (int i = 0; i < t.attack.count; i++) { T.att_dx[i] = (int8_t)t.attack.dx[i]; T.att_dy[i] = (int8_t)t.attack.dy[i]; }
             for (int i = 0; i < t.view.w * t.view.h; i++) T.view_mask[i] = t.view.in[i];
             p.feat_size[g] = feature_size(g);
-            if (t.view.w != gtype(0).view.w || t.view.h != gtype(0).view.h)
-                return fail("all groups must share one view size");
         }
-        // reward rules: one binary event (attack/kill/collide) between two 'any' symbols of
-        // different groups, receivers = the event's subject and/or object.
+        // reward rules: the common form (one attack/kill/collide event between 'any' agents of two
+        // groups, receivers among its subject/object) runs data-parallel (RuleParams); anything else
+        // goes through the DSL interpreter (DslProgram), rule order preserved either way.
         if ((int)rules.size() > kMaxRules) return fail("at most %d reward rules", kMaxRules);
-        p.n_rules = (int)rules.size();
-        for (size_t r = 0; r < rules.size(); r++) {
-            const Rule& R = rules[r];
-            if (R.on < 0 || R.on >= (int)nodes.size()) return fail("reward rule %zu: bad event node", r);
-            const Node& N = nodes[R.on];
-            int op;
-            if (N.op == kEvAttack) op = kOpAttack;
-            else if (N.op == kEvKill) op = kOpKill;
-            else if (N.op == kEvCollide) op = kOpCollide;
-            else return fail("reward rule %zu: only attack/kill/collide events are supported", r);
-            if (N.raw.size() < 2) return fail("reward rule %zu: malformed event", r);
-            const int sa = N.raw[0], sb = N.raw[1];
-            if (sa >= (int)syms.size() || sb >= (int)syms.size()) return fail("reward rule %zu: bad symbol", r);
-            if (syms[sa].index != -1 || syms[sb].index != -1 || syms[sa].group == syms[sb].group)
-                return fail("reward rule %zu: symbols must be 'any' agents of two different groups", r);
-            if ((int)R.recv.size() > kMaxRecv) return fail("reward rule %zu: too many receivers", r);
-            RuleParams& RP = p.rules[r];
-            RP.op = op; RP.subj_group = syms[sa].group; RP.obj_group = syms[sb].group;
-            RP.n_recv = (int)R.recv.size(); RP.terminal = R.terminal;
-            for (size_t k = 0; k < R.recv.size(); k++) {
-                if (R.recv[k] != sa && R.recv[k] != sb)
-                    return fail("reward rule %zu: receivers must be the event's subject or object", r);
-                RP.recv_is_obj[k] = R.recv[k] == sb;
-                RP.val[k] = R.val[k];
+        bool simple = true;
+        for (size_t r = 0; r < rules.size() && simple; r++) simple = simple_rule(rules[r]);
+        p.n_rules = 0;
+        p.dsl = 0;
+        if (simple) {
+            p.n_rules = (int)rules.size();
+            for (size_t r = 0; r < rules.size(); r++) {
+                const Rule& R = rules[r];
+                const Node& N = nodes[R.on];
+                const int sa = N.raw[0], sb = N.raw[1];
+                RuleParams& RP = p.rules[r];
+                RP.op = N.op == kEvAttack ? kOpAttack : (N.op == kEvKill ? kOpKill : kOpCollide);
+                RP.subj_group = syms[sa].group; RP.obj_group = syms[sb].group;
+                RP.n_recv = (int)R.recv.size(); RP.terminal = R.terminal;
+                for (size_t k = 0; k < R.recv.size(); k++) {
+                    RP.recv_is_obj[k] = R.recv[k] == sb;
+                    RP.val[k] = R.val[k];
+                }
             }
+        } else {
+            MFX_CHECK(compile_dsl(p.prog));
+            p.dsl = 1;
         }
         p.record_events = first_render ? 0 : 1;
         p.par_step = 1;
@@ -367,6 +527,8 @@ public:
                 alloc(s.cells, (size_t)E * W * H);
                 alloc(s.grp_n, (size_t)E * G); alloc(s.grp_dead, (size_t)E * G); alloc(s.grp_reward, (size_t)E * G);
                 alloc(s.id_counter, E); alloc(s.rng, E); alloc(s.n_atk, E); alloc(s.n_mov, E); alloc(s.done, E);
+                alloc(s.idx_mark, E);
+                MFX_HIP_THROW(hipMemset(s.grp_reward, 0, sizeof(float) * E * G));   // Group ctor
                 alloc(d_gp, 1); alloc(d_err, 1);
                 MFX_HIP_THROW(hipMemset(d_err, 0, sizeof(int32_t)));
                 s.err = d_err;
@@ -486,8 +648,12 @@ public:
         int total = 0, rowcap = 4, tcap = 1;
         for (int g = 0; g < G; g++) { total += tmpl_n[g]; rowcap = std::max(rowcap, tmpl_n[g]); tcap = std::max(tcap, tmpl_n[g]); }
         rowcap = (rowcap + 3) & ~3;                      // 16-B aligned rows (4 * 1183 floats)
-        for (int g = 0; g < G; g++)
+        for (int g = 0; g < G; g++) {
             if (gtype(g).n_action > 64) return fail("rollout: n_action must be <= 64");
+            if (gp.type[g].view_w != gp.type[0].view_w || gp.type[g].view_h != gp.type[0].view_h)
+                return fail("rollout: every group must share one view size; use the per-call API");
+        }
+        if (gp.dsl) return fail("rollout: reward rules outside the attack/kill/collide form need the per-call API");
         try {
             ensure_capacity(total, total);
             const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);

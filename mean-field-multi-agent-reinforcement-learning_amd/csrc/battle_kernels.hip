@@ -129,12 +129,11 @@ __global__ void __launch_bounds__(256) k_reset(const GameParams* __restrict__ gp
         const int x = c % W, y = c / W;
         cells[c] = (x == 0 || y == 0 || x == W - 1 || y == H - 1) ? kCellWall : kCellEmpty;
     }
-    if (TID < G) {
+    if (TID < G) {                 // Group::clear (GridWorld.h:281-284): the group reward survives
         s.grp_n[e * G + TID] = 0;
         s.grp_dead[e * G + TID] = 0;
-        s.grp_reward[e * G + TID] = 0.0f;
     }
-    if (TID == 0) { s.id_counter[e] = 0; s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = 0; }
+    if (TID == 0) { s.id_counter[e] = 0; s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = 0; s.idx_mark[e] = 0; }
 }
 
 __device__ __forceinline__ bool is_blank(const uint16_t* cells, int W, int H, int x, int y, int self) {
@@ -228,9 +227,10 @@ struct ObsSmem {                  // LDS carve-up of the observation kernels
 // integer division in the inner loops); kB = false is the generic path for any other config.
 struct BattleShape { static constexpr int VW = 13, VH = 13, NC = 7, G = 2, F = 34; };
 
+// Minimap of the observing group g: its own view size sets the scale (GridWorld.cc:338-340).
 template <bool kB>
-__device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView& v, const ObsSmem& sm) {
-    const TypeParams& T0 = gp.type[0];
+__device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int g) {
+    const TypeParams& T0 = gp.type[g];
     const int VW = kB ? BattleShape::VW : T0.view_w, VH = kB ? BattleShape::VH : T0.view_h;
     const int G = kB ? BattleShape::G : gp.n_groups, NV = VW * VH;
     const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
@@ -258,6 +258,8 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
     }
     __syncthreads();
 }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));   // nontemporal-storable float4
 
 // Fill the staging rows of agents [a0, a0+k) of group g, then stream them to out_view.
 template <bool kB>
@@ -335,12 +337,12 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     const int nf = k * VF;
     if ((((uintptr_t)dst) & 15) == 0) {
         const int n4 = nf >> 2;
-        const float4* src4 = reinterpret_cast<const float4*>(sm.stage);
-        float4* dst4 = reinterpret_cast<float4*>(dst);
-        for (int i = TID; i < n4; i += blockDim.x) dst4[i] = src4[i];
-        for (int i = (n4 << 2) + TID; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
+        const f32x4* src4 = reinterpret_cast<const f32x4*>(sm.stage);
+        f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+        for (int i = TID; i < n4; i += blockDim.x) __builtin_nontemporal_store(src4[i], dst4 + i);
+        for (int i = (n4 << 2) + TID; i < nf; i += blockDim.x) __builtin_nontemporal_store(sm.stage[i], dst + i);
     } else {
-        for (int i = TID; i < nf; i += blockDim.x) dst[i] = sm.stage[i];
+        for (int i = TID; i < nf; i += blockDim.x) __builtin_nontemporal_store(sm.stage[i], dst + i);
     }
     __syncthreads();
 }
@@ -440,16 +442,19 @@ __device__ __forceinline__ float wave_sum(float x) {         // fixed butterfly 
     return x;
 }
 
+// Observation rows are written once and read only by the caller (next kernel / host), never by
+// this launch: nontemporal (`nt`) stores keep them from displacing the env images in L2/MALL
+// (+7.5 % k_rollout throughput measured, profiles/r01_nt_store_ab.txt).
 // copy one staged 64-cell block (cells valid cells) to dst, 16-B aligned when cells == 64
 __device__ __forceinline__ void obs_flush(float* __restrict__ dst, const float* st, int lane, int cells) {
     constexpr int NC = BattleShape::NC;
     if (cells == kWaveCells) {
-        const float4* s4 = reinterpret_cast<const float4*>(st);
-        float4* d4 = reinterpret_cast<float4*>(dst);
-        d4[lane] = s4[lane];
-        if (lane < kWaveStageFloats / 4 - 64) d4[64 + lane] = s4[64 + lane];
+        const f32x4* s4 = reinterpret_cast<const f32x4*>(st);
+        f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+        __builtin_nontemporal_store(s4[lane], d4 + lane);
+        if (lane < kWaveStageFloats / 4 - 64) __builtin_nontemporal_store(s4[64 + lane], d4 + 64 + lane);
     } else {
-        for (int i = lane; i < cells * NC; i += 64) dst[i] = st[i];
+        for (int i = lane; i < cells * NC; i += 64) __builtin_nontemporal_store(st[i], dst + i);
     }
 }
 
@@ -491,7 +496,7 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
         const uint32_t pos = v.xy[id];
         if (f == emb + na + 1) val = (float)(int)(pos & 0xFFFF) / (float)W;
         if (f == emb + na + 2) val = (float)(int)(pos >> 16) / (float)H;
-        out_feat[p] = val;
+        __builtin_nontemporal_store(val, out_feat + p);
     }
 }
 
@@ -571,7 +576,7 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
         v.cells = lc;
     }
     obs_prologue(gp, sm, g);
-    obs_minimap<kB>(gp, v, sm);
+    obs_minimap<kB>(gp, v, sm, g);
     const TypeParams& T = gp.type[g];
     const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
     const int F = gp.feat_size[g];
@@ -986,15 +991,177 @@ __device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView&
     }
 }
 
+// ==================================================================================
+//  reward DSL (GridWorld::calc_reward + calc_rule + calc_event_node, RewardEngine.cc:216-443)
+// ==================================================================================
+// One lane walks the reference's DFS over agent bindings exactly: same level order
+// (RewardRule::input_symbols), same agent order, the same `involved` marks (meta bit 3) and the
+// same reward accumulation order.  Symbol bindings are agent ids (-1 = none).
+constexpr uint8_t kMetaInvolved = 8;
+
+__device__ __forceinline__ int dsl_agent_index(const EnvView& v, int mark, int id) {
+    // Agent::index: 0 from the constructor (GridWorld.h:139) until a clear_dead sets the list
+    // position (GridWorld.cc:718); positions do not move between two clear_dead calls.
+    if (id >= mark) return 0;
+    const int g = meta_group(v.meta[id]);
+    const uint16_t* ids = v.grp_ids + g * v.cap;
+    for (int i = 0; i < v.grp_n[g]; ++i)
+        if (ids[i] == id) return i;
+    return 0;
+}
+
+__device__ __forceinline__ bool dsl_bind(const DslSym& S, const EnvView& v, int mark, int ob) {
+    // AgentSymbol::bind_with_check (RewardEngine.cc:14-23)
+    if ((int)meta_group(v.meta[ob]) != S.group) return false;
+    return S.index == -1 || S.index == dsl_agent_index(v, mark, ob);
+}
+
+__device__ __forceinline__ bool dsl_leaf(const GameParams& gp, const DslNode& N, const EnvView& v, const int* ent) {
+    const DslProgram& P = gp.prog;
+    const DslSym& S = P.sym[N.a];
+    const bool all = S.index == -2;
+    const uint16_t* ids = v.grp_ids + S.group * v.cap;
+    const int n = all ? v.grp_n[S.group] : 1;
+    const int sub = ent[N.a];
+    switch (N.op) {
+        case kEvAttack: case kEvKill: case kEvCollide: {
+            const uint32_t want = N.op == kEvAttack ? kOpAttack : (N.op == kEvKill ? kOpKill : kOpCollide);
+            const int obj = ent[N.b];
+            for (int i = 0; i < n; ++i) {
+                const int id = all ? ids[i] : sub;
+                if (id < 0) return false;
+                if (!(meta_op(v.meta[id]) == want && v.op_obj[id] == obj)) return false;
+            }
+            return true;
+        }
+        case kEvAt: case kEvIn: {
+            for (int i = 0; i < n; ++i) {
+                const int id = all ? ids[i] : sub;
+                if (id < 0) return false;
+                const int x = (int)(v.xy[id] & 0xFFFF), y = (int)(v.xy[id] >> 16);
+                const bool in = N.op == kEvAt ? (x == N.i0 && y == N.i1)
+                                              : (x > N.i0 && x < N.i2 && y > N.i1 && y < N.i3);
+                if (!in) return false;
+            }
+            return true;
+        }
+        case kEvDie: {
+            for (int i = 0; i < n; ++i) {
+                const int id = all ? ids[i] : sub;
+                if (id < 0) return false;
+                if (!meta_dead(v.meta[id])) return false;
+            }
+            return true;
+        }
+        case kEvInALine: {                         // subject is 'all' (checked on the host)
+            const int m = v.grp_n[S.group];
+            if (m < 2) return true;
+            const int x0 = (int)(v.xy[ids[0]] & 0xFFFF), y0 = (int)(v.xy[ids[0]] >> 16);
+            const int dx = x0 - (int)(v.xy[ids[1]] & 0xFFFF), dy = y0 - (int)(v.xy[ids[1]] >> 16);
+            if ((dx == 0) == (dy == 0)) return false;
+            const bool vert = dx == 0;
+            int lo = vert ? y0 : x0, hi = lo;
+            bool line = true;
+            for (int i = 1; i < m && line; ++i) {
+                const int x = (int)(v.xy[ids[i]] & 0xFFFF), y = (int)(v.xy[ids[i]] >> 16);
+                const int c = vert ? y : x;
+                lo = c < lo ? c : lo; hi = c > hi ? c : hi;
+                line = vert ? x == x0 : y == y0;
+            }
+            return line && hi - lo + 1 == m;
+        }
+        default:
+            return false;
+    }
+}
+
+__device__ __forceinline__ bool dsl_eval(const GameParams& gp, const DslRule& R, const EnvView& v, const int* ent) {
+    const DslProgram& P = gp.prog;
+    uint32_t bits = 0;                          // AND / OR / NOT have no side effects: no short cut needed
+    for (int k = 0; k < R.n_post; ++k) {
+        const int ni = R.post[k];
+        const DslNode& N = P.node[ni];
+        bool r;
+        if (N.op == kEvAnd) r = ((bits >> N.a) & 1u) && ((bits >> N.b) & 1u);
+        else if (N.op == kEvOr) r = ((bits >> N.a) & 1u) || ((bits >> N.b) & 1u);
+        else if (N.op == kEvNot) r = !((bits >> N.a) & 1u);
+        else r = dsl_leaf(gp, N, v, ent);
+        bits |= (uint32_t)r << ni;
+    }
+    return (bits >> R.post[R.n_post - 1]) & 1u;
+}
+
+__device__ void dsl_rewards(const GameParams& gp, EnvView& v, int mark, int* flags) {
+    const DslProgram& P = gp.prog;
+    for (int r = 0; r < P.n_rules; ++r) {
+        const DslRule& R = P.rule[r];
+        int ent[kMaxSyms], it[kMaxSyms + 1], cur[kMaxSyms + 1];
+        for (int k = 0; k < kMaxSyms; ++k) ent[k] = -1;
+        int trig = 0, now = 0;
+        it[0] = 0; cur[0] = -1;
+        while (now >= 0) {
+            if (now == R.n_in) {                   // DFS last layer (RewardEngine.cc:376-390)
+                if (dsl_eval(gp, R, v, ent)) {
+                    trig = 1;
+                    for (int k = 0; k < R.n_recv; ++k) {
+                        const DslSym& S = P.sym[R.recv[k]];
+                        if (S.index == -2) v.grp_reward[S.group] += R.val[k];
+                        else v.next_r[ent[R.recv[k]]] += R.val[k];
+                    }
+                }
+                --now;
+                continue;
+            }
+            const int si = R.in_sym[now], inf = R.infer[now];
+            const DslSym& S = P.sym[si];
+            const uint16_t* ids = v.grp_ids + S.group * v.cap;
+            const int n = v.grp_n[S.group];
+            bool down = false;
+            if (S.index == -1) {                   // 'any': every agent not bound at a shallower level
+                if (cur[now] >= 0) { v.meta[cur[now]] &= (uint8_t)~kMetaInvolved; cur[now] = -1; }
+                while (!down && it[now] < n) {
+                    const int id = ids[it[now]++];
+                    ent[si] = id;
+                    if (v.meta[id] & kMetaInvolved) continue;
+                    v.meta[id] |= kMetaInvolved;
+                    cur[now] = id;
+                    if (inf < 0) { down = true; break; }
+                    const int ob = v.op_obj[id];
+                    if (ob >= 0 && dsl_bind(P.sym[inf], v, mark, ob)) { ent[inf] = ob; down = true; }
+                    else { v.meta[id] &= (uint8_t)~kMetaInvolved; cur[now] = -1; }
+                }
+            } else if (it[now] == 0) {             // 'all' / a fixed index: a single pass
+                it[now] = 1;
+                if (S.index == -2) {
+                    if (inf < 0) down = true;
+                    else if (n > 0) {
+                        const int ob = v.op_obj[ids[0]];
+                        if (ob >= 0 && dsl_bind(P.sym[inf], v, mark, ob)) { ent[inf] = ob; down = true; }
+                    }
+                } else if (S.index < n) {          // without an inference the reference stops here
+                    const int id = ids[S.index];
+                    ent[si] = id;
+                    const int ob = inf >= 0 ? v.op_obj[id] : -1;
+                    if (ob >= 0 && dsl_bind(P.sym[inf], v, mark, ob)) { ent[inf] = ob; down = true; }
+                }
+            }
+            if (down) { ++now; it[now] = 0; cur[now] = -1; }
+            else --now;
+        }
+        flags[r] = trig;
+    }
+}
+
 // Everything of GridWorld::step for one env, executed by the whole workgroup.
 // atk/mov/sorted: pending buffers (any address space); sorted has room for n_mov entries.
 // sm.tt must hold the serial type table (load_serial_types + barrier).
 // ps: LDS scratch for the parallel resolution (nullptr: one-lane loops only); nid = id_counter.
-template <bool kW>
+// kDsl: reward rules through the DSL interpreter (gp.dsl), dsl_mark = State::idx_mark of the env.
+template <bool kW, bool kDsl = false>
 __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
                               uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
                               int& done_out, const bool have_ps, const ParScratch ps, int nid,
-                              int32_t* ev = nullptr) {
+                              int32_t* ev = nullptr, int dsl_mark = 0) {
     const int G = gp.n_groups;
 #ifndef MFX_PAR_MASK
 #define MFX_PAR_MASK 3
@@ -1083,7 +1250,11 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         psync<kW>();
     }
     // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
-    for (int r = 0; r < gp.n_rules; ++r) {
+    if (kDsl) {
+        if (TID == 0) dsl_rewards(gp, v, dsl_mark, sm.flags);
+        psync<kW>();
+    }
+    for (int r = 0; r < (kDsl ? 0 : gp.n_rules); ++r) {
         const RuleParams& R = gp.rules[r];
         const int n = v.grp_n[R.subj_group];
         int obj_recv = 0;
@@ -1117,7 +1288,8 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         int live = 0;
         for (int g = 0; g < G; ++g) live += (v.grp_n[g] - v.grp_dead[g]) > 0;
         int d = live < G;
-        for (int r = 0; r < gp.n_rules; ++r) d |= sm.flags[r] && gp.rules[r].terminal;
+        if (kDsl) for (int r = 0; r < gp.prog.n_rules; ++r) d |= sm.flags[r] && gp.prog.rule[r].terminal;
+        else for (int r = 0; r < gp.n_rules; ++r) d |= sm.flags[r] && gp.rules[r].terminal;
         done_out = d;
     }
     psync<kW>();
@@ -1125,6 +1297,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
 
 // Copy an env into LDS, run the step, copy back.  When `lds` is 0 the env is worked on
 // in place in HBM (maps / agent counts too large for LDS).
+template <bool kDsl>
 __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp, State s, int lds,
                                               uint32_t* __restrict__ sort_scratch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1164,7 +1337,8 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     int done = 0;
     load_serial_types(gp, sm);
     int32_t* ev = (gp.record_events && e == 0) ? s.ev : nullptr;
-    step_env_core<false>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, false, ParScratch{}, nid, ev);
+    step_env_core<false, kDsl>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, false, ParScratch{}, nid, ev,
+                               kDsl ? s.idx_mark[e] : 0);
     if (lds) {
         for (int i = TID; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
         for (int i = TID; i < nid; i += blockDim.x) {
@@ -1217,6 +1391,7 @@ __global__ void __launch_bounds__(256) k_clear_dead(const GameParams* __restrict
     __shared__ int wave_tot[16];
     EnvView v = global_view(s, blockIdx.x, gp->n_groups);
     clear_dead_env<false>(*gp, v, wave_tot);
+    if (TID == 0) s.idx_mark[blockIdx.x] = s.id_counter[blockIdx.x];
 }
 
 // ==================================================================================
@@ -1511,7 +1686,11 @@ typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(1))) uint32_t g_u32;
 
 __device__ __forceinline__ uint4 ld_g16(const g_u32x4* p) {
+#ifdef MFX_NT_LD
+    const u32x4 x = __builtin_nontemporal_load(p);
+#else
     const u32x4 x = *p;
+#endif
     return make_uint4(x.x, x.y, x.z, x.w);
 }
 
@@ -1570,9 +1749,16 @@ __device__ __forceinline__ void pf_install(const EnvPrefetch& pf, char* image, E
 
 // 16-B copy by one wave (lane stride 64).
 __device__ __forceinline__ void wcopy16(void* dst, const void* src, size_t bytes, int lane) {
+#ifdef MFX_NT_WB
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    u32x4_t* d = reinterpret_cast<u32x4_t*>(dst);
+    const u32x4_t* q = reinterpret_cast<const u32x4_t*>(src);
+    for (size_t i = lane; i < (bytes >> 4); i += 64) __builtin_nontemporal_store(q[i], d + i);
+#else
     uint4* d = reinterpret_cast<uint4*>(dst);
     const uint4* q = reinterpret_cast<const uint4*>(src);
     for (size_t i = lane; i < (bytes >> 4); i += 64) d[i] = q[i];
+#endif
 }
 
 // Generic install (maps / capacities beyond the prefetch budget): straight copies.
@@ -1791,7 +1977,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GamePa
         MFX_STAMP(1);
         // ---------------- get_observation for every group
         obs_prologue(gp, osm, 0);
-        obs_minimap<kB>(gp, v, osm);
+        obs_minimap<kB>(gp, v, osm, 0);              // one view size for every group (rollout_plan)
         MFX_STAMP(2);
         for (int g = 0; g < G; ++g) {
             const TypeParams& T = gp.type[g];
@@ -1955,7 +2141,8 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
                        uint32_t* d_sort_scratch, hipStream_t st) {
     const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap);
     const int lds = smem <= 96 * 1024;
-    k_step<<<s.E, 256, lds ? smem : 0, st>>>(d_gp, s, lds, d_sort_scratch);
+    if (gp.dsl) k_step<true><<<s.E, 256, lds ? smem : 0, st>>>(d_gp, s, lds, d_sort_scratch);
+    else k_step<false><<<s.E, 256, lds ? smem : 0, st>>>(d_gp, s, lds, d_sort_scratch);
     return hipGetLastError();
 }
 

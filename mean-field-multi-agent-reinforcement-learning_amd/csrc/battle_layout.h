@@ -12,7 +12,8 @@
 //     last_r    f32 [E][cap]   Agent::last_reward
 //     last_act  u8  [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145)
 //     op_obj    i32 [E][cap]   id of Agent::op_obj or -1
-//     meta      u8  [E][cap]   bit0 dead | bits1-2 last_op | bits4-5 group
+//     meta      u8  [E][cap]   bit0 dead | bits1-2 last_op | bit3 involved (reward DSL, transient)
+//                              | bits4-5 group
 //   groups
 //     grp_ids   u16 [E][G][cap] the ordered agent vector of each group (Group::agents)
 //     grp_n, grp_dead i32 [E][G];  grp_reward f32 [E][G]
@@ -30,7 +31,9 @@ constexpr int kMaxGroups = 4;
 constexpr int kMaxViewCells = 32 * 32;
 constexpr int kMaxRangeCount = 64;
 constexpr int kMaxRules = 8;
-constexpr int kMaxRecv = 4;
+constexpr int kMaxRecv = 8;
+constexpr int kMaxSyms = 16;        // reward DSL: agent symbols, event nodes (RewardEngine.h)
+constexpr int kMaxNodes = 32;
 constexpr uint16_t kCellEmpty = 0xFFFF;
 constexpr uint16_t kCellWall = 0xFFFE;
 constexpr uint32_t kBucketBoundary = 0xFF;
@@ -38,7 +41,8 @@ constexpr uint32_t kBucketBoundary = 0xFF;
 // last_op encoding in meta bits 1-2
 enum : uint32_t { kOpNull = 0, kOpAttack = 1, kOpKill = 2, kOpCollide = 3 };
 // reference EventOp numbering (grid_def.h:17-23), used by the reward-rule ABI
-enum : int { kEvKill = 3, kEvCollide = 6, kEvAttack = 7 };
+enum : int { kEvAnd = 0, kEvOr = 1, kEvNot = 2, kEvKill = 3, kEvAt = 4, kEvIn = 5, kEvCollide = 6, kEvAttack = 7,
+             kEvDie = 8, kEvInALine = 9, kEvAlign = 10 };
 
 struct TypeParams {                 // AgentType (AgentType.h:17-52), the fields the path reads
     float hp, damage, step_recover, kill_supply;
@@ -62,6 +66,28 @@ struct RuleParams {                 // RewardRule on one binary event between tw
     int terminal;
 };
 
+// The general reward DSL (RewardEngine.cc:105-443), compiled on the host into the reference's
+// own inference plan (init_reward_description) and interpreted by one lane per env (k_step<true>).
+struct DslSym { int group, index; };                 // index -1 any, -2 all, >= 0 fixed
+struct DslNode {                                     // op (kEv*); a, b: node or symbol numbers;
+    int op, a, b, i0, i1, i2, i3;                    // i0..i3: AT (x, y) / IN (x1, y1, x2, y2)
+};
+struct DslRule {
+    int n_in;                                        // DFS levels (RewardRule::input_symbols)
+    int8_t in_sym[kMaxSyms], infer[kMaxSyms];        // infer: symbol bound from op_obj, or -1
+    int n_post;                                      // the `on` subtree, children before parents
+    int8_t post[kMaxNodes];
+    int n_recv, terminal;
+    int8_t recv[kMaxRecv];
+    float val[kMaxRecv];
+};
+struct DslProgram {
+    int n_rules;
+    DslSym sym[kMaxSyms];
+    DslNode node[kMaxNodes];
+    DslRule rule[kMaxRules];
+};
+
 struct GameParams {
     int W, H, n_groups, minimap, emb, n_ch;
     int large_map, n_sep, band_w;
@@ -69,9 +95,11 @@ struct GameParams {
     int record_events;              // 1 once rendering started: k_step records env 0's attack events
     int par_step;                   // 1: attack / move resolution may run in parallel (every
                                     //    kill_supply == 0, so a kill never changes the killer's hp)
+    int dsl;                        // 1: reward rules outside the RuleParams form run through `prog`
     int feat_size[kMaxGroups];
     TypeParams type[kMaxGroups];    // per group (Group::type)
     RuleParams rules[kMaxRules];
+    DslProgram prog;
 };
 
 struct State {                      // device pointers; every array is [E][stride]
@@ -95,6 +123,8 @@ struct State {                      // device pointers; every array is [E][strid
     uint32_t* mov;                  // [E][acap]
     int32_t* n_mov;                 // [E]
     int32_t* done;                  // [E]
+    int32_t* idx_mark;              // [E] id_counter at the last clear_dead: Agent::index is the list
+                                    //     position for ids below it, else 0 (GridWorld.h:139, :718)
     int32_t* err;                   // [1] sticky device-side error code
     int32_t* ev;                    // [1 + 3 * acap] env 0's attack events of the last step (render):
                                     //   count, then (attacker id, target x, target y) in shuffle order

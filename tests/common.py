@@ -28,6 +28,16 @@ def pin_ref_threads():
     ctypes.CDLL("libgomp.so.1").omp_set_num_threads(1)
 
 
+def config_env(lib_path, config, map_size):
+    """A drop-in GridWorld on lib_path for a builtin config name or a magent Config."""
+    import magent
+    if os.path.abspath(lib_path) == os.path.abspath(REF_LIB):
+        pin_ref_threads()
+    lib = magent.load_library(lib_path)
+    env = magent.GridWorld(config, map_size=map_size, lib=lib)
+    return env, env.get_handles()
+
+
 def battle_env(lib_path, map_size):
     import magent
     if os.path.abspath(lib_path) == os.path.abspath(REF_LIB):

@@ -1,0 +1,130 @@
+"""the reference's other builtin configs (forest, double_attack) and the
+general reward DSL (RewardEngine.cc:216-443: attack / kill / collide / at / in / die / in_a_line,
+and / or / not, 'any' / 'all' / fixed-index symbols, group receivers, terminal rules) on the HIP
+engine, step for step against the reference build (oracle/_ref) on the same seeded scenario:
+views, features, rewards, alive flags, positions, ids and done after every step."""
+import os
+
+import numpy as np
+import pytest
+
+import common
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.path.exists(common.REF_LIB), reason="oracle/_ref not built")]
+
+
+def _play(lib_path, config, map_size, counts, seed, steps, walls, episodes=2):
+    env, handles = common.config_env(lib_path, config, map_size)
+    env.set_seed(seed)
+    rs = np.random.RandomState(seed)
+    out = []
+    for ep in range(episodes):
+        env.reset()
+        env.add_walls(method="random", n=walls)
+        for h, n in zip(handles, counts):
+            env.add_agents(h, method="random", n=n)
+        for t in range(steps):
+            rec = []
+            for h in handles:
+                view, feat = env.get_observation(h)
+                rec += [view.copy(), feat.copy()]
+            for h in handles:
+                n_act = env.get_action_space(h)[0]
+                env.set_action(h, rs.randint(0, n_act, env.get_num(h)).astype(np.int32))
+            done = env.step()
+            for h in handles:
+                rec += [env.get_reward(h).copy(), env.get_alive(h).copy(), env.get_pos(h).copy(),
+                        env.get_agent_id(h).copy()]
+            rec.append(np.array([done]))
+            out.append(rec)
+            if t % 3 == 2:            # leave agents un-cleared for a while: Agent::index stays 0
+                env.clear_dead()
+            if done:
+                break
+    del env
+    return out
+
+
+def _compare(got, ref):
+    assert len(got) == len(ref), "episode lengths differ: %d vs %d" % (len(got), len(ref))
+    for t, (a, b) in enumerate(zip(got, ref)):
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert x.shape == y.shape and x.tobytes() == y.tobytes(), "step %d field %d differs" % (t, k)
+
+
+def _both(config, map_size, counts, seed, steps=40, walls=10):
+    ref = _play(common.REF_LIB, config, map_size, counts, seed, steps, walls)
+    got = _play(common.HIP_LIB, config, map_size, counts, seed, steps, walls)
+    _compare(got, ref)
+    return ref
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_forest_matches_reference(seed):
+    """builtin/config/forest.py: per-group view sizes (3x3 deer, 9x9 tigers), no attack actions for
+    deer, starving tigers (step_recover < 0), kill_supply > 0 (serial attack path)."""
+    _both("forest", 20, (40, 30), seed)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_double_attack_matches_reference(seed):
+    """builtin/config/double_attack.py: Event(a, attack, c) & Event(b, attack, c) over two 'any' tiger
+    symbols -- the DFS with `involved` marks and re-bound inferred objects."""
+    ref = _both("double_attack", 14, (30, 60), seed, steps=60)
+    assert any(np.any(r[8] > 0.5) for r in ref), "no double attack happened: the test is vacuous"
+
+
+def _dsl_config(map_size, variant):
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": map_size, "map_height": map_size, "embedding_size": 6, "minimap_mode": variant % 2 == 1})
+    a_t = cfg.register_agent_type("a", dict(width=1, length=1, hp=6, speed=1, view_range=gw.CircleRange(3),
+                                            attack_range=gw.CircleRange(1.5), damage=2, step_recover=0.1,
+                                            attack_in_group=1, step_reward=-0.01, kill_reward=1,
+                                            dead_penalty=-0.5, attack_penalty=-0.05))
+    b_t = cfg.register_agent_type("b", dict(width=1, length=1, hp=4, speed=2, view_range=gw.CircleRange(3),
+                                            attack_range=gw.CircleRange(1), damage=1, step_recover=-0.05,
+                                            kill_supply=1, step_reward=0.01))
+    g0, g1 = cfg.add_group(a_t), cfg.add_group(b_t)
+    a, a2 = gw.AgentSymbol(g0, "any"), gw.AgentSymbol(g0, "any")
+    b = gw.AgentSymbol(g1, "any")
+    all_a, all_b = gw.AgentSymbol(g0, "all"), gw.AgentSymbol(g1, "all")
+    first_a, third_b = gw.AgentSymbol(g0, 0), gw.AgentSymbol(g1, 2)
+    E = gw.Event
+    if variant == 0:
+        cfg.add_reward_rule(E(a, "attack", b) | E(a, "kill", b), receiver=[a, b], value=[0.3, -0.2])
+        cfg.add_reward_rule(E(a, "attack", a2), receiver=a2, value=-1.0)           # same-group, attack_in_group
+        cfg.add_reward_rule(E(b, "collide", a) & ~E(a, "attack", b), receiver=[b, all_a], value=[0.5, 0.01])
+        cfg.add_reward_rule(E(b, "die"), receiver=[b, all_b], value=[-3.0, -0.02])
+        cfg.add_reward_rule(E(a, "in", ((2, 2), (map_size // 2, map_size // 2))), receiver=a, value=0.07)
+        cfg.add_reward_rule(E(b, "at", (map_size // 2, map_size // 2)), receiver=b, value=9.0)
+    else:
+        cfg.add_reward_rule(E(first_a, "attack", b), receiver=[first_a, b], value=[2.0, -2.0])   # fixed index
+        cfg.add_reward_rule(E(a, "attack", third_b), receiver=[a, third_b], value=[1.5, -1.5])   # bind index check
+        cfg.add_reward_rule(E(all_a, "attack", b), receiver=all_a, value=0.25)                   # 'all' subject
+        cfg.add_reward_rule(E(all_b, "in_a_line"), receiver=all_b, value=0.125)
+        cfg.add_reward_rule(E(a, "kill", b) | E(b, "collide", a), receiver=[all_a, a], value=[4.0, 0.5])
+        cfg.add_reward_rule(E(all_b, "die"), receiver=all_a, value=8.0, terminal=True)
+        cfg.add_reward_rule(E(b, "collide", b), receiver=b, value=0.2)
+    return cfg
+
+
+@pytest.mark.parametrize("variant,seed", [(0, 3), (0, 4), (1, 5), (1, 6)])
+def test_reward_dsl_matches_reference(variant, seed):
+    _both(_dsl_config(16, variant), 16, (36, 28), seed, steps=50, walls=8)
+
+
+def test_in_a_line_all_subject_small_group():
+    """in_a_line on a group of <= 2 agents and a terminal rule that fires on the first step."""
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": 10, "map_height": 10})
+    t = cfg.register_agent_type("t", dict(width=1, length=1, hp=3, speed=1, view_range=gw.CircleRange(2),
+                                          attack_range=gw.CircleRange(1), damage=1))
+    g0, g1 = cfg.add_group(t), cfg.add_group(t)
+    cfg.add_reward_rule(gw.Event(gw.AgentSymbol(g1, "all"), "in_a_line"), receiver=gw.AgentSymbol(g1, "all"),
+                        value=1.0, terminal=True)
+    _both(cfg, 10, (5, 2), 7, steps=5, walls=2)
