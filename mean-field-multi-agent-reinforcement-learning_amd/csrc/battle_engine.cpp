@@ -218,7 +218,8 @@ public:
                 continue;
             return fail("invalid agent config in register_agent_type: %s", k);
         }
-        if (t.width != 1 || t.length != 1) return fail("only 1x1 agent bodies are supported");
+        if (t.width < 1 || t.length < 1 || t.width > 8 || t.length > 8)
+            return fail("agent bodies must be 1..8 cells wide and long");
         if (t.can_absorb) return fail("can_absorb is not supported");
         const int parity = t.width % 2;
         if (t.view_angle >= 180) {
@@ -436,6 +437,7 @@ public:
             T.view_x1 = t.width / 2 + t.view.x1;     // eye = pos + view offset (Map.cc:146-149)
             T.view_y1 = t.length / 2 + t.view.y1;
             T.att_x_off = t.width / 2; T.att_y_off = t.length / 2;
+            T.body_w = t.width; T.body_h = t.length;
             for (int i = 0; i < t.move.count; i++) { T.move_dx[i] = (int8_t)t.move.dx[i]; T.move_dy[i] = (int8_t)t.move.dy[i]; }
             for (int i = 0; i < t.attack.count; i++) { T.att_dx[i] = (int8_t)t.attack.dx[i]; T.att_dy[i] = (int8_t)t.attack.dy[i]; }
             for (int i = 0; i < t.view.w * t.view.h; i++) T.view_mask[i] = t.view.in[i];
@@ -470,7 +472,8 @@ public:
         }
         p.record_events = first_render ? 0 : 1;
         p.par_step = 1;
-        for (int g = 0; g < p.n_groups; g++) p.par_step &= p.type[g].kill_supply == 0.0f;
+        for (int g = 0; g < p.n_groups; g++)
+            p.par_step &= p.type[g].kill_supply == 0.0f && p.type[g].body_w == 1 && p.type[g].body_h == 1;
         gp = p;
         return 0;
     }
@@ -654,6 +657,8 @@ public:
                 return fail("rollout: every group must share one view size; use the per-call API");
         }
         if (gp.dsl) return fail("rollout: reward rules outside the attack/kill/collide form need the per-call API");
+        for (int g = 0; g < G; g++)
+            if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return fail("rollout: 1x1 bodies only; use the per-call API");
         try {
             ensure_capacity(total, total);
             const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);

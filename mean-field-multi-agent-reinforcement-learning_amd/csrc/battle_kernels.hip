@@ -143,6 +143,35 @@ __device__ __forceinline__ bool is_blank(const uint16_t* cells, int W, int H, in
     return c == kCellEmpty || (int)c == self;
 }
 
+// Bodies of bw x bh cells (width x length; every agent faces NORTH without turn_mode).
+__device__ __forceinline__ bool is_blank_area(const uint16_t* cells, int W, int H, int x, int y, int bw, int bh,
+                                              int self) {
+    if (x < 0 || y < 0 || x + bw >= W || y + bh >= H) return false;
+    for (int i = 0; i < bw; ++i)
+        for (int j = 0; j < bh; ++j) {
+            const uint32_t c = cells[(y + j) * W + x + i];
+            if (!(c == kCellEmpty || (int)c == self)) return false;
+        }
+    return true;
+}
+
+__device__ __forceinline__ void fill_area(uint16_t* cells, int W, int x, int y, int bw, int bh, uint16_t val) {
+    for (int i = 0; i < bw; ++i)
+        for (int j = 0; j < bh; ++j) cells[(y + j) * W + x + i] = val;
+}
+
+// Map::get_collide (Map.cc:498-513): the first other agent of the rectangle, column by column.
+__device__ __forceinline__ int get_collide(const uint16_t* cells, int W, int H, int x, int y, int bw, int bh,
+                                           int self) {
+    if (x < 0 || y < 0 || x + bw >= W || y + bh >= H) return -1;
+    for (int i = 0; i < bw; ++i)
+        for (int j = 0; j < bh; ++j) {
+            const uint32_t c = cells[(y + j) * W + x + i];
+            if (c < kCellWall && (int)c != self) return (int)c;
+        }
+    return -1;
+}
+
 // One lane per env: placements are order-dependent (an occupied cell is skipped and the
 // id is not consumed -- GridWorld.cc:180-187).  method: 0 custom, 1 random, 2 fill.
 __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int group, int n, int method,
@@ -162,11 +191,11 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
             if (c == kCellEmpty || c == kCellWall) c = kCellWall;
             return;
         }
-        if (!is_blank(v.cells, W, H, x, y, -1)) return;
-        if (idc >= s.cap || idc >= 0xFFFE) { set_err(s, 2); return; }
         const TypeParams& T = gp->type[group];
+        if (!is_blank_area(v.cells, W, H, x, y, T.body_w, T.body_h, -1)) return;
+        if (idc >= s.cap || idc >= 0xFFFE) { set_err(s, 2); return; }
         const int id = idc++;
-        v.cells[y * W + x] = (uint16_t)id;
+        fill_area(v.cells, W, x, y, T.body_w, T.body_h, (uint16_t)id);
         v.xy[id] = (uint32_t)x | ((uint32_t)y << 16);
         v.hp[id] = T.hp;
         v.last_r[id] = 0.0f;                                     // Agent ctor + init_reward()
@@ -181,19 +210,21 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
     if (method == 0) {
         for (int i = 0; i < n; ++i) place(px[i], py[i]);
     } else if (method == 1) {                                    // Map::get_random_blank (Map.cc:49-63)
+        const int bw = group < 0 ? 1 : gp->type[group].body_w, bh = group < 0 ? 1 : gp->type[group].body_h;
         for (int i = 0; i < n; ++i) {
             int x = 0, y = 0, tries = 0;
             for (;;) {
-                rng = minstd_next(rng); x = (int)(rng % (uint32_t)(W - 1));
-                rng = minstd_next(rng); y = (int)(rng % (uint32_t)(H - 1));
-                if (is_blank(v.cells, W, H, x, y, -1)) break;
+                rng = minstd_next(rng); x = (int)(rng % (uint32_t)(W - bw));
+                rng = minstd_next(rng); y = (int)(rng % (uint32_t)(H - bh));
+                if (is_blank_area(v.cells, W, H, x, y, bw, bh, -1)) break;
                 if (tries++ > W * H) { set_err(s, 3); break; }
             }
             place(x, y);
         }
-    } else {                                                     // fill: xs = {x, y, w, h}
-        for (int x = px[0]; x < px[0] + px[2]; ++x)
-            for (int y = px[1]; y < px[1] + px[3]; ++y) place(x, y);
+    } else {                                                     // fill: xs = {x, y, w, h}, body strides
+        const int bw = group < 0 ? 1 : gp->type[group].body_w, bh = group < 0 ? 1 : gp->type[group].body_h;
+        for (int x = px[0]; x < px[0] + px[2]; x += bw)
+            for (int y = px[1]; y < px[1] + px[3]; y += bh) place(x, y);
     }
     s.rng[e] = rng;
     s.id_counter[e] = idc;
@@ -503,6 +534,7 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
 __host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
     if (gp.n_groups != BattleShape::G || !gp.minimap || gp.n_ch != BattleShape::NC) return false;
     for (int g = 0; g < gp.n_groups; ++g) {
+        if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return false;
         if (gp.type[g].view_w != BattleShape::VW || gp.type[g].view_h != BattleShape::VH ||
             gp.feat_size[g] != BattleShape::F || gp.type[g].view_x1 != gp.type[0].view_x1 ||
             gp.type[g].view_y1 != gp.type[0].view_y1)
@@ -651,6 +683,7 @@ struct SerialType {          // what the one-lane loops read per group, kept in 
     float hp, damage, kill_supply, kill_reward, dead_penalty, attack_penalty;   // index is
     int attack_in_group, att_x_off, att_y_off, pad;                              // lane-varying:
     int n_attack, turn_base, attack_base, n_action;
+    int body_w, body_h, pad2[2];
     int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];                       // from global it
     int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];                     // would be a vector
 };                                                                               // load per use)
@@ -676,6 +709,7 @@ __device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem
             S.attack_in_group = T.attack_in_group; S.att_x_off = T.att_x_off; S.att_y_off = T.att_y_off;
             S.n_attack = T.n_attack; S.turn_base = T.turn_base; S.attack_base = T.attack_base;
             S.n_action = T.n_action;
+            S.body_w = T.body_w; S.body_h = T.body_h;
         }
     }
 }
@@ -715,7 +749,8 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, const Ste
             v.next_r[cv] = OT.dead_penalty;
             m = meta_make(0, kOpKill, g);
             v.op_obj[id] = (int)cv;
-            v.cells[oy * W + ox] = kCellEmpty;                                      // remove_agent
+            const uint32_t vp = v.xy[cv];                                           // remove_agent
+            fill_area(v.cells, W, (int)(vp & 0xFFFF), (int)(vp >> 16), OT.body_w, OT.body_h, kCellEmpty);
             v.grp_dead[og] += 1;
             const float h2 = v.hp[id] + OT.kill_supply;                             // add_hp
             v.hp[id] = T.hp < h2 ? T.hp : h2;
@@ -739,15 +774,29 @@ __device__ __forceinline__ void do_move_one(const GameParams& gp, const StepSmem
     const uint32_t p = v.xy[id];
     const int x = p & 0xFFFF, y = p >> 16;
     const int nx = x + T.move_dx[mi], ny = y + T.move_dy[mi];
-    if (nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) return;     // out of board: no collide
-    const uint32_t cv = v.cells[ny * W + nx];
-    if (cv == kCellEmpty || (int)cv == id) {
-        v.cells[y * W + x] = kCellEmpty;
-        v.cells[ny * W + nx] = (uint16_t)id;
+    if (T.body_w == 1 && T.body_h == 1) {
+        if (nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) return;     // out of board: no collide
+        const uint32_t cv = v.cells[ny * W + nx];
+        if (cv == kCellEmpty || (int)cv == id) {
+            v.cells[y * W + x] = kCellEmpty;
+            v.cells[ny * W + nx] = (uint16_t)id;
+            v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
+        } else if (cv != kCellWall) {
+            v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(m));
+            v.op_obj[id] = (int)cv;
+        }
+        return;
+    }
+    if (is_blank_area(v.cells, W, H, nx, ny, T.body_w, T.body_h, id)) {
+        fill_area(v.cells, W, x, y, T.body_w, T.body_h, kCellEmpty);
+        fill_area(v.cells, W, nx, ny, T.body_w, T.body_h, (uint16_t)id);
         v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
-    } else if (cv != kCellWall) {
-        v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(m));
-        v.op_obj[id] = (int)cv;
+    } else {
+        const int c = get_collide(v.cells, W, H, nx, ny, T.body_w, T.body_h, id);
+        if (c >= 0) {
+            v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(m));
+            v.op_obj[id] = c;
+        }
     }
 }
 
@@ -1210,7 +1259,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
                     v.meta[id] = (uint8_t)(m | 1u);
                     v.next_r[id] = T.dead_penalty;
                     const uint32_t p = v.xy[id];
-                    v.cells[(p >> 16) * gp.W + (p & 0xFFFF)] = kCellEmpty;
+                    fill_area(v.cells, gp.W, (int)(p & 0xFFFF), (int)(p >> 16), T.body_w, T.body_h, kCellEmpty);
                     atomicAdd(&v.grp_dead[g], 1);
                 }
             }

@@ -52,6 +52,7 @@ struct TypeParams {                 // AgentType (AgentType.h:17-52), the fields
     int n_move, n_attack;
     int view_w, view_h, view_x1, view_y1;      // view window relative to the agent (NORTH)
     int att_x_off, att_y_off;
+    int body_w, body_h;                        // width x length cells from pos (NORTH, Map.cc:75-97)
     int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];
     int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];
     uint8_t view_mask[kMaxViewCells];          // Range::is_in, row-major [view_h][view_w]

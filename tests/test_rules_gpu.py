@@ -128,3 +128,59 @@ def test_in_a_line_all_subject_small_group():
     cfg.add_reward_rule(gw.Event(gw.AgentSymbol(g1, "all"), "in_a_line"), receiver=gw.AgentSymbol(g1, "all"),
                         value=1.0, terminal=True)
     _both(cfg, 10, (5, 2), 7, steps=5, walls=2)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_pursuit_matches_reference(seed):
+    """builtin/config/pursuit.py: 2x2 predators -- multi-cell placement (random and blank checks),
+    moves that overlap the mover's own body, collisions (first other agent column by column),
+    attacks landing on any cell of a body, removal of whole bodies, views of multi-cell agents --
+    and speed-1.5 prey."""
+    ref = _both("pursuit", 20, (12, 40), seed, steps=60)
+    assert any(np.any(r[4] > 0.5) for r in ref), "no predator hit a prey: the test is vacuous"
+
+
+def test_odd_bodies_fill_and_custom_placement():
+    """2x3 and 3x1 bodies placed by 'fill' (body-size strides) and 'custom' (overlaps skipped), with
+    minimap mode, starvation removing whole bodies and a kill-triggered rule."""
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": 18, "map_height": 18, "minimap_mode": True, "embedding_size": 5})
+    big = cfg.register_agent_type("big", dict(width=2, length=3, hp=5, speed=1, view_range=gw.CircleRange(3),
+                                              attack_range=gw.CircleRange(2), damage=2, step_recover=-0.3,
+                                              kill_reward=2))
+    long_ = cfg.register_agent_type("long", dict(width=3, length=1, hp=3, speed=2, view_range=gw.CircleRange(2),
+                                                 attack_range=gw.CircleRange(1.5), damage=1, kill_supply=1))
+    g0, g1 = cfg.add_group(big), cfg.add_group(long_)
+    a, b = gw.AgentSymbol(g0, "any"), gw.AgentSymbol(g1, "any")
+    cfg.add_reward_rule(gw.Event(a, "kill", b) | gw.Event(b, "kill", a), receiver=[a, b], value=[1.0, 1.0])
+
+    def run(lib_path):
+        env, (h0, h1) = common.config_env(lib_path, cfg, 18)
+        env.set_seed(9)
+        rs = np.random.RandomState(9)
+        env.reset()
+        env.add_agents(h0, method="fill", pos=[2, 2], size=[7, 9])
+        env.add_agents(h1, method="custom", pos=[[10, 3], [11, 3], [10, 5], [12, 8], [3, 3], [14, 12], [9, 14]])
+        env.add_agents(h1, method="fill", pos=[10, 10], size=[6, 3])
+        out = []
+        for t in range(40):
+            rec = []
+            for h in (h0, h1):
+                view, feat = env.get_observation(h)
+                rec += [view.copy(), feat.copy()]
+            for h in (h0, h1):
+                env.set_action(h, rs.randint(0, env.get_action_space(h)[0], env.get_num(h)).astype(np.int32))
+            done = env.step()
+            for h in (h0, h1):
+                rec += [env.get_reward(h).copy(), env.get_alive(h).copy(), env.get_pos(h).copy()]
+            rec.append(np.array([done]))
+            out.append(rec)
+            env.clear_dead()
+            if done:
+                break
+        del env
+        return out
+
+    _compare(run(common.HIP_LIB), run(common.REF_LIB))
