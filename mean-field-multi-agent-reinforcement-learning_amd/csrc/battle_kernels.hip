@@ -499,9 +499,9 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
     const uint16_t* ids = v.grp_ids + g * v.cap;
     const float* mm_own = sm.mm + g * NV;
     const float* mm_en = sm.mm + (g ^ 1) * NV;
-    float* st = wave_stage + wid * kWaveStageFloats;
     const int ncell = n * NV;
     for (int base = wid * 2 * kWaveCells; base < ncell; base += nw * 2 * kWaveCells) {
+        float* st = wave_stage + wid * kWaveStageFloats;
         const CellObs o0 = obs_cell(v, sm, mm_own, mm_en, W, H, g, base + lane, ncell);
         obs_stage_cell(st, lane, o0);
         wave_sync_lds();
@@ -1536,6 +1536,9 @@ __device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-o
 #ifndef MFX_ROLLOUT_THREADS
 #define MFX_ROLLOUT_THREADS 256
 #endif
+#ifndef MFX_ROLLOUT_OCC
+#define MFX_ROLLOUT_OCC 5          // workgroups per CU the register budget is sized for
+#endif
 // LDS plan of k_rollout: the env (cells, per-id arrays, group lists) stays resident for the whole
 // launch; one scratch region is shared by the observation phase (minimap, bins, hp/max, staging) and
 // the policy/step phase (actions, histogram, attack/move buffers; the reduction reuses the actions).
@@ -1930,7 +1933,7 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
 // fits on the chip at once, and each workgroup takes envs from a work queue, keeping env e in LDS
 // while the next env's image is already in flight into registers.
 template <bool kB, bool kPf>
-__global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, 5) k_rollout(const GameParams* __restrict__ gpp,
+__global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollout(const GameParams* __restrict__ gpp,
                                                                  const RolloutCtx* __restrict__ ctx,
                                                                  uint32_t step_index, int work_sel, int qphase) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
