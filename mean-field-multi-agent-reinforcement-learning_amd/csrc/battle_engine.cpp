@@ -131,7 +131,7 @@ public:
     int pending_ub = 0;                              // upper bound of queued actions
     // drop-in staging (env 0, host buffers)
     DevBuf<float> st_view, st_feat, st_f32;
-    DevBuf<int> st_i32, st_xs, st_ys;
+    DevBuf<int> st_i32, st_xs, st_ys, st_dirs;
     DevBuf<uint8_t> st_u8;
     // fused rollout (bench / throughput path)
     bool rollout_ready = false;
@@ -154,7 +154,7 @@ public:
         for (void* p : {(void*)s.cells, (void*)s.xy, (void*)s.hp, (void*)s.next_r, (void*)s.last_r,
                         (void*)s.last_act, (void*)s.op_obj, (void*)s.meta, (void*)s.grp_ids, (void*)s.grp_n,
                         (void*)s.grp_dead, (void*)s.grp_reward, (void*)s.id_counter, (void*)s.rng, (void*)s.atk,
-                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)s.idx_mark, (void*)d_sort, (void*)d_gp,
+                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)s.idx_mark, (void*)s.food, (void*)d_sort, (void*)d_gp,
                         (void*)d_err})
             if (p) (void)hipFree(p);
         s = State{}; d_sort = nullptr; d_gp = nullptr; d_err = nullptr; allocated = false;
@@ -190,7 +190,6 @@ public:
                 MFX_HIP(hipStreamSynchronize(stream));
             }
         } else return fail("invalid argument in set_config: %s", key);
-        if (food || turn || goal) return fail("food_mode/turn_mode/goal_mode are not supported (DESIGN.md scope)");
         return 0;
     }
 
@@ -232,7 +231,7 @@ public:
         } else t.attack = sector_range(t.attack_angle, t.attack_radius, parity);
         t.move = circle_range(t.speed, 0, 1);
         t.turn_base = t.move.count;
-        t.attack_base = t.turn_base;
+        t.attack_base = turn ? t.turn_base + 2 : t.turn_base;      // AgentType.cc:118-122 (turn at register)
         t.n_action = t.attack_base + t.attack.count;
         if (t.view.w * t.view.h > kMaxViewCells || t.view.w <= 0 || t.view.h <= 0)
             return fail("view range too large (max %d cells)", kMaxViewCells);
@@ -422,6 +421,7 @@ public:
         if (G == 0) return fail("no groups");
         GameParams p{};
         p.W = W; p.H = H; p.n_groups = G; p.minimap = minimap; p.emb = emb;
+        p.turn_mode = turn; p.food_mode = food;
         p.n_ch = group2channel(G);
         if ((long)W * H > 99 * 99) { large_map = true; n_sep = (long)W * H > 1000 * 1000 ? 16 : 8; }  // sticky
         p.large_map = large_map; p.n_sep = n_sep; p.band_w = (W + n_sep - 1) / n_sep;
@@ -438,6 +438,9 @@ public:
             T.view_y1 = t.length / 2 + t.view.y1;
             T.att_x_off = t.width / 2; T.att_y_off = t.length / 2;
             T.body_w = t.width; T.body_h = t.length;
+            T.view_off_x = t.width / 2; T.view_off_y = t.length / 2;
+            T.view_lt_x = t.view.x1; T.view_lt_y = t.view.y1;
+            T.eat_ability = t.eat_ability; T.food_supply = t.food_supply;
             for (int i = 0; i < t.move.count; i++) { T.move_dx[i] = (int8_t)t.move.dx[i]; T.move_dy[i] = (int8_t)t.move.dy[i]; }
             for (int i = 0; i < t.attack.count; i++) { T.att_dx[i] = (int8_t)t.attack.dx[i]; T.att_dy[i] = (int8_t)t.attack.dy[i]; }
             for (int i = 0; i < t.view.w * t.view.h; i++) T.view_mask[i] = t.view.in[i];
@@ -474,6 +477,7 @@ public:
         p.par_step = 1;
         for (int g = 0; g < p.n_groups; g++)
             p.par_step &= p.type[g].kill_supply == 0.0f && p.type[g].body_w == 1 && p.type[g].body_h == 1;
+        if (turn || food) p.par_step = 0;
         gp = p;
         return 0;
     }
@@ -499,7 +503,7 @@ public:
         if (need_ids > s.cap) {
             int nc = std::max(64, s.cap);
             while (nc < need_ids) nc *= 2;
-            if (nc > 0xFFFE) nc = 0xFFFE;
+            if (nc > kCellFood) nc = kCellFood;        // ids stay below the cell codes
             const int oc = s.cap;
             grow(s.xy, E, oc, nc); grow(s.hp, E, oc, nc); grow(s.next_r, E, oc, nc); grow(s.last_r, E, oc, nc);
             grow(s.last_act, E, oc, nc); grow(s.op_obj, E, oc, nc); grow(s.meta, E, oc, nc);
@@ -531,6 +535,7 @@ public:
                 alloc(s.grp_n, (size_t)E * G); alloc(s.grp_dead, (size_t)E * G); alloc(s.grp_reward, (size_t)E * G);
                 alloc(s.id_counter, E); alloc(s.rng, E); alloc(s.n_atk, E); alloc(s.n_mov, E); alloc(s.done, E);
                 alloc(s.idx_mark, E);
+                if (food) alloc(s.food, (size_t)E * W * H);
                 MFX_HIP_THROW(hipMemset(s.grp_reward, 0, sizeof(float) * E * G));   // Group ctor
                 alloc(d_gp, 1); alloc(d_err, 1);
                 MFX_HIP_THROW(hipMemset(d_err, 0, sizeof(int32_t)));
@@ -543,6 +548,7 @@ public:
             } else if (s.cells_n != W * H) {
                 return fail("map size changed after the first reset");
             }
+            if (food && !s.food) alloc(s.food, (size_t)E * W * H);
             MFX_HIP_THROW(hipMemcpyAsync(d_gp, &gp, sizeof(GameParams), hipMemcpyHostToDevice, stream));
             MFX_HIP_THROW(launch_reset(d_gp, s, stream));
             next_file();                              // GridWorld.cc:102
@@ -556,19 +562,27 @@ public:
     }
 
     // same placement for every env (host arrays)
-    int add_agents(int group, int n, const char* method, const int* xs, const int* ys) {
+    int add_agents(int group, int n, const char* method, const int* xs, const int* ys, const int* dirs) {
         if (!allocated) return fail("add_agents before reset");
         if (group >= n_groups() || group < -1) return fail("invalid group handle in add_agents: %d", group);
         int m, count;
-        std::vector<int> hx, hy;
+        std::vector<int> hx, hy, hd;
         if (!strcmp(method, "custom")) {
             m = 0; count = n;
             hx.assign(xs, xs + n); hy.assign(ys, ys + n);
+            if (group >= 0) {                                  // GridWorld.cc:259-261
+                hd.assign((size_t)n, kDirNorth);
+                for (int i = 0; i < n && dirs; i++) {
+                    if (dirs[i] >= 4) return fail("invalid direction in GridWorld::add_agent");
+                    hd[i] = dirs[i];
+                }
+            }
         } else if (!strcmp(method, "random")) {
             m = 1; count = n;
         } else if (!strcmp(method, "fill")) {
             m = 2; count = std::max(0, xs[2]) * std::max(0, xs[3]);
-            hx.assign(xs, xs + 4);
+            hx.assign(xs, xs + (turn && group >= 0 ? 5 : 4));   // {x, y, w, h, dir} (GridWorld.cc:270-273)
+            if (turn && group >= 0 && (hx[4] < 0 || hx[4] >= 4)) return fail("invalid direction in GridWorld::add_agent");
         } else return fail("unsupported method in add_agents: %s", method);
         try {
             if (group >= 0) {
@@ -578,15 +592,26 @@ public:
             }
             if (hx.empty()) hx.push_back(0);
             if (hy.empty()) hy.push_back(0);
-            st_xs.ensure(hx.size()); st_ys.ensure(hy.size());
+            if (hd.empty()) hd.push_back(kDirNorth);
+            st_xs.ensure(hx.size()); st_ys.ensure(hy.size()); st_dirs.ensure(hd.size());
             MFX_HIP_THROW(hipMemcpyAsync(st_xs.p, hx.data(), sizeof(int) * hx.size(), hipMemcpyHostToDevice, stream));
             MFX_HIP_THROW(hipMemcpyAsync(st_ys.p, hy.data(), sizeof(int) * hy.size(), hipMemcpyHostToDevice, stream));
-            MFX_HIP_THROW(launch_add_agents(d_gp, s, group, n, m, st_xs.p, st_ys.p, 0, stream));
+            MFX_HIP_THROW(hipMemcpyAsync(st_dirs.p, hd.data(), sizeof(int) * hd.size(), hipMemcpyHostToDevice, stream));
+            MFX_HIP_THROW(launch_add_agents(d_gp, s, group, n, m, st_xs.p, st_ys.p, st_dirs.p, 0, stream));
             MFX_HIP_THROW(hipStreamSynchronize(stream));   // host vectors go out of scope
             return check_err();
         } catch (const HipFailure& f) {
             return fail("%s", f.what());
         }
+    }
+
+    // GridWorld::set_goal (GridWorld.cc:729-740): "random" only, goals never read back.
+    int set_goal(int group, const char* method) {
+        if (strcmp(method, "random")) return fail("invalid goal type in GridWorld::set_goal");
+        if (!allocated || group < 0 || group >= n_groups()) return fail("set_goal: bad state or group");
+        MFX_HIP(launch_set_goal_random(d_gp, s, group, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        return 0;
     }
 
     int check_err() {
@@ -657,6 +682,7 @@ public:
                 return fail("rollout: every group must share one view size; use the per-call API");
         }
         if (gp.dsl) return fail("rollout: reward rules outside the attack/kill/collide form need the per-call API");
+        if (turn || food) return fail("rollout: turn_mode / food_mode need the per-call API");
         for (int g = 0; g < G; g++)
             if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return fail("rollout: 1x1 bodies only; use the per-call API");
         try {
@@ -700,7 +726,7 @@ public:
             return fail("%s", f.what());
         }
         MFX_CHECK(reset());
-        for (int g = 0; g < G; g++) MFX_CHECK(add_agents(g, tmpl_n[g], "custom", xs[g], ys[g]));
+        for (int g = 0; g < G; g++) MFX_CHECK(add_agents(g, tmpl_n[g], "custom", xs[g], ys[g], nullptr));
         MFX_CHECK(rollout_plan());
         rollout_ready = true;
         return 0;
@@ -935,17 +961,19 @@ public:
             for (int i = 0; i < G && allocated; i++) {
                 const int n = num_env0(i);
                 if (!n) continue;
-                std::vector<int> ids(n), pos(2 * (size_t)n);
+                std::vector<int> ids(n), pos(2 * (size_t)n), dir(n);
                 std::vector<float> hp(n);
                 MFX_CHECK(host_get(i, kGetId, ids.data(), 4));
                 MFX_CHECK(host_get(i, kGetPos, pos.data(), 8));
                 MFX_CHECK(host_get(i, kGetHp, hp.data(), 4));
+                MFX_CHECK(host_get(i, kGetDir, dir.data(), 4));
                 const float max_hp = gtype(i).hp;
+                static const int dir2angle[] = {0, 90, 180, 270};   // RenderGenerator.cc:148
                 for (int j = 0; j < n; j++) {
                     int h = std::max(0, int(100 * hp[j] / max_hp));
                     h = std::min(h, 100);
-                    fout << ids[j] << " " << h << " " << 270 << " " << pos[2 * j] << " " << pos[2 * j + 1] << " " << i
-                         << std::endl;                    // dir2angle[NORTH] = 270 (turn mode off)
+                    fout << ids[j] << " " << h << " " << dir2angle[dir[j] & 3] << " " << pos[2 * j] << " "
+                         << pos[2 * j + 1] << " " << i << std::endl;
                 }
             }
             for (size_t k = 0; k < ev.size(); k += 3)
@@ -1093,16 +1121,15 @@ MFX_API int gridworld_new_group(void* game, const char* agent_type_name, int* gr
 }
 MFX_API int gridworld_add_agents(void* game, int group, int n, const char* method, const int* pos_x, const int* pos_y,
                                  const int* dir) {
-    (void)dir;   // turn_mode is off: every agent faces NORTH (GridWorld.cc:264)
-    MFX_GUARD(MFX_ENV(game)->add_agents(group, n, method, pos_x, pos_y));
+    MFX_GUARD(MFX_ENV(game)->add_agents(group, n, method, pos_x, pos_y, dir));
 }
 MFX_API int gridworld_clear_dead(void* game) {
     BattleEngine* e = MFX_ENV(game);
     MFX_GUARD(e->clear_dead() ? -1 : (hipStreamSynchronize(e->stream) == hipSuccess ? 0 : -1));
 }
 MFX_API int gridworld_set_goal(void* game, int group, const char* method, const int* linear_buffer) {
-    (void)game; (void)group; (void)method; (void)linear_buffer;
-    return mfx::fail("set_goal is deprecated in the reference and not supported");
+    (void)linear_buffer;
+    MFX_GUARD(MFX_ENV(game)->set_goal(group, method));
 }
 MFX_API int gridworld_define_agent_symbol(void* game, int no, int group, int index) {
     BattleEngine* e = MFX_ENV(game);

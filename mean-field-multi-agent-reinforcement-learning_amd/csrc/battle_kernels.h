@@ -6,14 +6,15 @@
 
 namespace mfx {
 
-enum GetWhat : int { kGetNum = 0, kGetReward = 1, kGetId = 2, kGetAlive = 3, kGetPos = 4, kGetHp = 5, kGetLastAct = 6 };
+enum GetWhat : int { kGetNum = 0, kGetReward = 1, kGetId = 2, kGetAlive = 3, kGetPos = 4, kGetHp = 5, kGetLastAct = 6, kGetDir = 7 };
 
 size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n, int cap);
 size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap);
 
 hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st);
 hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
-                             const int* d_xs, const int* d_ys, int per_env_stride, hipStream_t st);
+                             const int* d_xs, const int* d_ys, const int* d_dirs, int per_env_stride, hipStream_t st);
+hipError_t launch_set_goal_random(const GameParams* d_gp, const State& s, int g, hipStream_t st);
 hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
                           float* d_view, float* d_feat, int rowcap, hipStream_t st);
 hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, const int* d_actions, int rowcap,

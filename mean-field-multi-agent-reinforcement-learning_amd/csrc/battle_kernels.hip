@@ -100,6 +100,7 @@ struct EnvView {
     int32_t* op_obj;
     uint8_t* meta;
     uint16_t* grp_ids;     // [G][cap]
+    float* food;           // [H*W] food amounts (food_mode) or null; always in HBM
     int32_t* grp_n;        // [G]
     int32_t* grp_dead;     // [G]
     float* grp_reward;     // [G]
@@ -113,6 +114,7 @@ __device__ __forceinline__ EnvView global_view(const State& s, int e, int G) {
     v.xy = s.xy + a; v.hp = s.hp + a; v.next_r = s.next_r + a; v.last_r = s.last_r + a;
     v.last_act = s.last_act + a; v.op_obj = s.op_obj + a; v.meta = s.meta + a;
     v.grp_ids = s.grp_ids + (size_t)e * G * s.cap;
+    v.food = s.food ? s.food + (size_t)e * s.cells_n : nullptr;
     v.grp_n = s.grp_n + e * G; v.grp_dead = s.grp_dead + e * G; v.grp_reward = s.grp_reward + e * G;
     v.cap = s.cap;
     return v;
@@ -167,15 +169,43 @@ __device__ __forceinline__ int get_collide(const uint16_t* cells, int W, int H, 
     for (int i = 0; i < bw; ++i)
         for (int j = 0; j < bh; ++j) {
             const uint32_t c = cells[(y + j) * W + x + i];
-            if (c < kCellWall && (int)c != self) return (int)c;
+            if (c < kCellFood && (int)c != self) return (int)c;
         }
     return -1;
+}
+
+// Direction geometry (Map.cc:530-612): rela_to_abs, save_to_real, real_to_save, get_size_for_dir.
+__device__ __forceinline__ void rela_to_abs(int cx, int cy, int dir, int rx, int ry, int& ax, int& ay) {
+    if (dir == kDirNorth) { ax = cx + rx; ay = cy + ry; }
+    else if (dir == kDirSouth) { ax = cx - rx; ay = cy - ry; }
+    else if (dir == kDirWest) { ax = cx + ry; ay = cy - rx; }
+    else { ax = cx - ry; ay = cy + rx; }
+}
+
+__device__ __forceinline__ void save_to_real(int px, int py, int dir, int w, int l, int& rx, int& ry) {
+    if (dir == kDirNorth) { rx = px; ry = py; }
+    else if (dir == kDirSouth) { rx = px + w - 1; ry = py + l - 1; }
+    else if (dir == kDirWest) { rx = px; ry = py + w - 1; }
+    else { rx = px + l - 1; ry = py; }
+}
+
+__device__ __forceinline__ void real_to_save(int rx, int ry, int dir, int w, int l, int& px, int& py) {
+    if (dir == kDirNorth) { px = rx; py = ry; }
+    else if (dir == kDirSouth) { px = rx - w + 1; py = ry - l + 1; }
+    else if (dir == kDirWest) { px = rx; py = ry - w + 1; }
+    else { px = rx - l + 1; py = ry; }
+}
+
+__device__ __forceinline__ void size_for_dir(int dir, int w, int l, int& bw, int& bh) {
+    const bool ns = dir == kDirNorth || dir == kDirSouth;
+    bw = ns ? w : l; bh = ns ? l : w;
 }
 
 // One lane per env: placements are order-dependent (an occupied cell is skipped and the
 // id is not consumed -- GridWorld.cc:180-187).  method: 0 custom, 1 random, 2 fill.
 __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int group, int n, int method,
-                             const int* __restrict__ xs, const int* __restrict__ ys, int per_env_stride) {
+                             const int* __restrict__ xs, const int* __restrict__ ys, const int* __restrict__ dirs,
+                             int per_env_stride) {
     const int e = blockIdx.x * blockDim.x + TID;
     if (e >= s.E) return;
     const int W = gp->W, H = gp->H, G = gp->n_groups;
@@ -184,7 +214,7 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
     const int* py = ys + (size_t)e * per_env_stride;
     uint32_t rng = s.rng[e];
     int idc = s.id_counter[e];
-    auto place = [&](int x, int y) {
+    auto place = [&](int x, int y, int dir) {
         if (group < 0) {                                         // Map::add_wall (Map.cc:108-115)
             if (x < 0 || y < 0 || x >= W || y >= H) return;
             uint16_t& c = v.cells[y * W + x];
@@ -192,26 +222,32 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
             return;
         }
         const TypeParams& T = gp->type[group];
-        if (!is_blank_area(v.cells, W, H, x, y, T.body_w, T.body_h, -1)) return;
-        if (idc >= s.cap || idc >= 0xFFFE) { set_err(s, 2); return; }
+        int bw, bh;
+        size_for_dir(dir, T.body_w, T.body_h, bw, bh);               // Map::add_agent (Map.cc:75-97)
+        if (!is_blank_area(v.cells, W, H, x, y, bw, bh, -1)) return;
+        if (idc >= s.cap || idc >= kCellFood) { set_err(s, 2); return; }
         const int id = idc++;
-        fill_area(v.cells, W, x, y, T.body_w, T.body_h, (uint16_t)id);
+        fill_area(v.cells, W, x, y, bw, bh, (uint16_t)id);
         v.xy[id] = (uint32_t)x | ((uint32_t)y << 16);
         v.hp[id] = T.hp;
         v.last_r[id] = 0.0f;                                     // Agent ctor + init_reward()
         v.next_r[id] = T.step_reward;
         v.last_act[id] = T.n_action;
         v.op_obj[id] = -1;
-        v.meta[id] = (uint8_t)meta_make(0, kOpNull, group);
+        v.meta[id] = (uint8_t)meta_set_dir(meta_make(0, kOpNull, group), dir);
         int& n = v.grp_n[group];
         v.grp_ids[group * s.cap + n] = (uint16_t)id;
         ++n;
     };
+    const bool turn = group >= 0 && gp->turn_mode;
     if (method == 0) {
-        for (int i = 0; i < n; ++i) place(px[i], py[i]);
+        for (int i = 0; i < n; ++i) place(px[i], py[i], turn ? dirs[(size_t)e * per_env_stride + i] : kDirNorth);
     } else if (method == 1) {                                    // Map::get_random_blank (Map.cc:49-63)
-        const int bw = group < 0 ? 1 : gp->type[group].body_w, bh = group < 0 ? 1 : gp->type[group].body_h;
         for (int i = 0; i < n; ++i) {
+            int dir = kDirNorth;
+            if (turn) { rng = minstd_next(rng); dir = (int)(rng % 4u); }   // GridWorld.cc:241
+            int bw = 1, bh = 1;
+            if (group >= 0) size_for_dir(dir, gp->type[group].body_w, gp->type[group].body_h, bw, bh);
             int x = 0, y = 0, tries = 0;
             for (;;) {
                 rng = minstd_next(rng); x = (int)(rng % (uint32_t)(W - bw));
@@ -219,12 +255,14 @@ __global__ void k_add_agents(const GameParams* __restrict__ gp, State s, int gro
                 if (is_blank_area(v.cells, W, H, x, y, bw, bh, -1)) break;
                 if (tries++ > W * H) { set_err(s, 3); break; }
             }
-            place(x, y);
+            place(x, y, dir);
         }
-    } else {                                                     // fill: xs = {x, y, w, h}, body strides
-        const int bw = group < 0 ? 1 : gp->type[group].body_w, bh = group < 0 ? 1 : gp->type[group].body_h;
+    } else {                                                     // fill: xs = {x, y, w, h, dir}, body strides
+        const int dir = turn ? px[4] : kDirNorth;
+        int bw = 1, bh = 1;
+        if (group >= 0) size_for_dir(dir, gp->type[group].body_w, gp->type[group].body_h, bw, bh);
         for (int x = px[0]; x < px[0] + px[2]; x += bw)
-            for (int y = px[1]; y < px[1] + px[3]; y += bh) place(x, y);
+            for (int y = px[1]; y < px[1] + px[3]; y += bh) place(x, y, dir);
     }
     s.rng[e] = rng;
     s.id_counter[e] = idc;
@@ -304,6 +342,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
     const int NV = VW * VH, VF = NV * NC;
     const bool MM = kB ? true : gp.minimap != 0;
     const int per = MM ? 3 : 2;
+    const int cbase = (!kB && gp.food_mode) ? 2 : 1;     // group2channel(0) (GridWorld.cc:999-1008)
     const uint16_t* ids = v.grp_ids + g * v.cap;
     // ---- phase 1: one lane per (agent, view cell) computes that cell's NC channels
     for (int p = TID; p < k * NV; p += blockDim.x) {
@@ -314,14 +353,23 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
         float o[kMaxCh];
 #pragma unroll
         for (int q = 0; q < kMaxCh; ++q) o[q] = 0.0f;
-        const int mx = (int)(pos & 0xFFFF) + T.view_x1 + vx, my = (int)(pos >> 16) + T.view_y1 + vy;
+        int mx = (int)(pos & 0xFFFF) + T.view_x1 + vx, my = (int)(pos >> 16) + T.view_y1 + vy;
+        if (!kB && gp.turn_mode) {                      // Map::extract_view (Map.cc:130-218) as a gather
+            const int dir = meta_dir(v.meta[id]);
+            int rx, ry, ex, ey;
+            save_to_real((int)(pos & 0xFFFF), (int)(pos >> 16), dir, T.body_w, T.body_h, rx, ry);
+            rela_to_abs(rx, ry, dir, T.view_off_x, T.view_off_y, ex, ey);
+            rela_to_abs(ex, ey, dir, T.view_lt_x + vx, T.view_lt_y + vy, mx, my);
+        }
         if (sm.mask[c] && mx >= 0 && my >= 0 && mx < W && my < H) {
             const uint32_t cv = v.cells[my * W + mx];
             if (cv == kCellWall) {
                 o[0] = 1.0f;
+            } else if (cv == kCellFood) {
+                o[1] = 1.0f;                               // food_channel_id (Map.h:35), no hp
             } else if (cv != kCellEmpty) {
                 const int og = meta_group(v.meta[cv]);
-                const int ch = 1 + per * ((og - g + G) % G);
+                const int ch = cbase + per * ((og - g + G) % G);
                 const float hn = v.hp[cv] / sm.type_hp[og];
 #pragma unroll
                 for (int q = 0; q < kMaxCh; ++q) {
@@ -334,7 +382,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
             const bool self = c == (int)sm.bin[id];
             for (int j = 0; j < G; ++j) {
                 const float m = sm.mm[j * NV + c];
-                const int ch = 3 + per * ((j - g + G) % G);
+                const int ch = cbase + 2 + per * ((j - g + G) % G);
 #pragma unroll
                 for (int q = 0; q < kMaxCh; ++q)
                     if (q == ch) o[q] = self ? m + 1.0f : m;
@@ -419,7 +467,7 @@ __device__ __forceinline__ CellObs obs_cell(const EnvView& v, const ObsSmem& sm,
     const int mx = (int)(int16_t)(q.x & 0xFFFFu) + vx, my = ((int)q.x >> 16) + vy;
     const bool ok = valid && mk != 0 && (unsigned)mx < (unsigned)W && (unsigned)my < (unsigned)H;
     const uint32_t cv = v.cells[ok ? my * W + mx : 0];
-    const bool agent = ok && cv < kCellWall;
+    const bool agent = ok && cv < kCellFood;
     const uint32_t inf = sm.info[agent ? cv : 0];
     CellObs o;
     o.mo = valid ? (self ? mo + 1.0f : mo) : 0.0f;
@@ -532,7 +580,8 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
 }
 
 __host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
-    if (gp.n_groups != BattleShape::G || !gp.minimap || gp.n_ch != BattleShape::NC) return false;
+    if (gp.n_groups != BattleShape::G || !gp.minimap || gp.n_ch != BattleShape::NC || gp.turn_mode || gp.food_mode)
+        return false;
     for (int g = 0; g < gp.n_groups; ++g) {
         if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return false;
         if (gp.type[g].view_w != BattleShape::VW || gp.type[g].view_h != BattleShape::VH ||
@@ -645,7 +694,7 @@ __device__ __forceinline__ void set_action_group(const GameParams& gp, const Sta
             a = acts[i];
             if (a < 0 || a >= T.n_action) { set_err(s, 5); a = T.turn_base > 6 ? 6 : 0; }
             v.last_act[id] = a;
-            is_move = a < T.turn_base;
+            is_move = a < T.attack_base;                  // moves and turns (same buckets, GridWorld.cc:443-470)
             is_atk = !is_move;
             if (is_move && gp.large_map) {
                 const int x = v.xy[id] & 0xFFFF, xr = x % gp.band_w;
@@ -683,7 +732,8 @@ struct SerialType {          // what the one-lane loops read per group, kept in 
     float hp, damage, kill_supply, kill_reward, dead_penalty, attack_penalty;   // index is
     int attack_in_group, att_x_off, att_y_off, pad;                              // lane-varying:
     int n_attack, turn_base, attack_base, n_action;
-    int body_w, body_h, pad2[2];
+    int body_w, body_h;
+    float eat_ability, food_supply;
     int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];                       // from global it
     int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];                     // would be a vector
 };                                                                               // load per use)
@@ -710,6 +760,7 @@ __device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem
             S.n_attack = T.n_attack; S.turn_base = T.turn_base; S.attack_base = T.attack_base;
             S.n_action = T.n_action;
             S.body_w = T.body_w; S.body_h = T.body_h;
+            S.eat_ability = T.eat_ability; S.food_supply = T.food_supply;
         }
     }
 }
@@ -727,8 +778,14 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, const Ste
         const int g = meta_group(m);
         const SerialType& T = sm.tt[g];
         const uint32_t p = v.xy[id];
-        const int ox = (int)(p & 0xFFFF) + T.att_x_off + T.att_dx[ai];
-        const int oy = (int)(p >> 16) + T.att_y_off + T.att_dy[ai];
+        int ox = (int)(p & 0xFFFF) + T.att_x_off + T.att_dx[ai];
+        int oy = (int)(p >> 16) + T.att_y_off + T.att_dy[ai];
+        if (gp.turn_mode) {                            // Map::get_attack_obj (Map.cc:220-263)
+            const int dir = meta_dir(m);
+            int rx, ry;
+            save_to_real((int)(p & 0xFFFF), (int)(p >> 16), dir, T.body_w, T.body_h, rx, ry);
+            rela_to_abs(rx, ry, dir, T.att_x_off + T.att_dx[ai], T.att_y_off + T.att_dy[ai], ox, oy);
+        }
         if (ev) {
             const int k = ev[0];
             ev[1 + 3 * k] = id; ev[2 + 3 * k] = ox; ev[3 + 3 * k] = oy;
@@ -737,6 +794,16 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, const Ste
         uint32_t cv = kCellEmpty;
         if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
         if (cv >= kCellWall) { v.next_r[id] += T.attack_penalty; continue; }       // blank
+        if (cv == kCellFood) {                       // Map::do_attack, OCC_FOOD (Map.cc:296-307)
+            float& f = v.food[oy * W + ox];
+            const float add = T.eat_ability < f ? T.eat_ability : f;
+            const float h2 = v.hp[id] + add;
+            v.hp[id] = T.hp < h2 ? T.hp : h2;
+            f -= add;
+            if ((double)f < 0.1) v.cells[oy * W + ox] = kCellEmpty;
+            v.next_r[id] += 0.0f + T.attack_penalty;
+            continue;
+        }
         const uint32_t om = v.meta[cv];
         const int og = meta_group(om);
         if (!T.attack_in_group && og == g) { v.next_r[id] += T.attack_penalty; continue; }
@@ -745,18 +812,24 @@ __device__ __forceinline__ void do_attack_serial(const GameParams& gp, const Ste
         const float ohp = v.hp[cv] - T.damage;                                    // Agent::be_attack
         v.hp[cv] = ohp;
         if (ohp < 0.0f) {
-            v.meta[cv] = (uint8_t)meta_make(1, meta_op(om), og);
+            v.meta[cv] = (uint8_t)meta_keep_dir(meta_make(1, meta_op(om), og), om);
             v.next_r[cv] = OT.dead_penalty;
-            m = meta_make(0, kOpKill, g);
+            m = meta_keep_dir(meta_make(0, kOpKill, g), m);
             v.op_obj[id] = (int)cv;
             const uint32_t vp = v.xy[cv];                                           // remove_agent
-            fill_area(v.cells, W, (int)(vp & 0xFFFF), (int)(vp >> 16), OT.body_w, OT.body_h, kCellEmpty);
+            int vbw, vbh;
+            size_for_dir(meta_dir(om), OT.body_w, OT.body_h, vbw, vbh);
+            fill_area(v.cells, W, (int)(vp & 0xFFFF), (int)(vp >> 16), vbw, vbh, kCellEmpty);
+            if (gp.food_mode) {                                                     // Map.cc:287-294
+                v.cells[oy * W + ox] = kCellFood;
+                v.food[oy * W + ox] = OT.food_supply;
+            }
             v.grp_dead[og] += 1;
             const float h2 = v.hp[id] + OT.kill_supply;                             // add_hp
             v.hp[id] = T.hp < h2 ? T.hp : h2;
             reward = OT.kill_reward;
         } else {
-            m = meta_make(0, kOpAttack, g);
+            m = meta_keep_dir(meta_make(0, kOpAttack, g), m);
             v.op_obj[id] = (int)cv;
         }
         v.meta[id] = (uint8_t)m;
@@ -773,7 +846,13 @@ __device__ __forceinline__ void do_move_one(const GameParams& gp, const StepSmem
     const SerialType& T = sm.tt[meta_group(m)];
     const uint32_t p = v.xy[id];
     const int x = p & 0xFFFF, y = p >> 16;
-    const int nx = x + T.move_dx[mi], ny = y + T.move_dy[mi];
+    if (mi >= T.turn_base) return;                 // a turn (turn_mode): done before the moves
+    int dx = T.move_dx[mi], dy = T.move_dy[mi];
+    const int dir = meta_dir(m);                   // GridWorld.cc:640-652
+    if (dir == kDirSouth) { dx = -dx; dy = -dy; }
+    else if (dir == kDirWest) { const int t = dx; dx = dy; dy = -t; }
+    else if (dir == kDirEast) { const int t = dx; dx = -dy; dy = t; }
+    const int nx = x + dx, ny = y + dy;
     if (T.body_w == 1 && T.body_h == 1) {
         if (nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) return;     // out of board: no collide
         const uint32_t cv = v.cells[ny * W + nx];
@@ -781,22 +860,55 @@ __device__ __forceinline__ void do_move_one(const GameParams& gp, const StepSmem
             v.cells[y * W + x] = kCellEmpty;
             v.cells[ny * W + nx] = (uint16_t)id;
             v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
-        } else if (cv != kCellWall) {
-            v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(m));
+        } else if (cv < kCellFood) {
+            v.meta[id] = (uint8_t)meta_keep_dir(meta_make(0, kOpCollide, meta_group(m)), m);
             v.op_obj[id] = (int)cv;
         }
         return;
     }
-    if (is_blank_area(v.cells, W, H, nx, ny, T.body_w, T.body_h, id)) {
-        fill_area(v.cells, W, x, y, T.body_w, T.body_h, kCellEmpty);
-        fill_area(v.cells, W, nx, ny, T.body_w, T.body_h, (uint16_t)id);
+    int bw, bh;
+    size_for_dir(dir, T.body_w, T.body_h, bw, bh);
+    if (is_blank_area(v.cells, W, H, nx, ny, bw, bh, id)) {
+        fill_area(v.cells, W, x, y, bw, bh, kCellEmpty);
+        fill_area(v.cells, W, nx, ny, bw, bh, (uint16_t)id);
         v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
     } else {
-        const int c = get_collide(v.cells, W, H, nx, ny, T.body_w, T.body_h, id);
+        const int c = get_collide(v.cells, W, H, nx, ny, bw, bh, id);
         if (c >= 0) {
-            v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(m));
+            v.meta[id] = (uint8_t)meta_keep_dir(meta_make(0, kOpCollide, meta_group(m)), m);
             v.op_obj[id] = c;
         }
+    }
+}
+
+// Map::do_turn (Map.cc:372-410) as the step calls it: the action a in [turn_base, attack_base) turns by
+// wise = 2a - 1 (GridWorld.cc:605), so the new direction is (dir + 2a - 1) mod 4 and, wise never
+// being -1, the body pivots with the clockwise formula about its real corner (turn offsets are 0).
+__device__ __forceinline__ void do_turn_one(const GameParams& gp, const StepSmem& sm, EnvView& v, uint32_t ent) {
+    const int id = (int)(ent >> 16), a = (int)((ent >> 8) & 0xFF);
+    const uint32_t m = v.meta[id];
+    if (meta_dead(m)) return;
+    const SerialType& T = sm.tt[meta_group(m)];
+    if (a < T.turn_base) return;                   // a move
+    const int W = gp.W, H = gp.H;
+    const int wise = 2 * a - 1;
+    const int dir = meta_dir(m), ndir = (dir + wise + 4) % 4;
+    int bw, bh;
+    size_for_dir(dir, T.body_w, T.body_h, bw, bh);
+    const uint32_t p = v.xy[id];
+    const int x = (int)(p & 0xFFFF), y = (int)(p >> 16);
+    int rx, ry, ax, ay;
+    save_to_real(x, y, dir, T.body_w, T.body_h, rx, ry);
+    rela_to_abs(rx, ry, dir, 0, 0, ax, ay);        // anchor: turn_x_offset = turn_y_offset = 0
+    const int ddx = rx - ax, ddy = ry - ay;
+    const int nrx = ax + ddy, nry = ay - ddx;
+    int sx, sy;
+    real_to_save(nrx, nry, ndir, T.body_w, T.body_h, sx, sy);
+    if (is_blank_area(v.cells, W, H, sx, sy, bh, bw, id)) {
+        fill_area(v.cells, W, x, y, bw, bh, kCellEmpty);
+        v.meta[id] = (uint8_t)meta_set_dir(m, ndir);
+        fill_area(v.cells, W, sx, sy, bh, bw, (uint16_t)id);
+        v.xy[id] = (uint32_t)sx | ((uint32_t)sy << 16);
     }
 }
 
@@ -916,7 +1028,7 @@ __device__ void attack_parallel(const GameParams& gp, const StepSmem& sm, EnvVie
             uint32_t cv = kCellEmpty;
             if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
             T = -1;
-            if (cv < kCellWall && (S.attack_in_group || (int)meta_group(v.meta[cv]) != g)) T = (int)cv;
+            if (cv < kCellFood && (S.attack_in_group || (int)meta_group(v.meta[cv]) != g)) T = (int)cv;
             ps.dmg[t] = S.damage;
         }
         ps.att[t] = (uint16_t)A;
@@ -1025,7 +1137,7 @@ __device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView&
                     v.cells[src] = kCellEmpty;
                     v.cells[dst] = (uint16_t)id;
                     v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
-                } else if (cv != kCellWall) {
+                } else if (cv < kCellFood) {
                     v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(v.meta[id]));
                     v.op_obj[id] = (int)cv;
                 }
@@ -1259,7 +1371,9 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
                     v.meta[id] = (uint8_t)(m | 1u);
                     v.next_r[id] = T.dead_penalty;
                     const uint32_t p = v.xy[id];
-                    fill_area(v.cells, gp.W, (int)(p & 0xFFFF), (int)(p >> 16), T.body_w, T.body_h, kCellEmpty);
+                    int bw, bh;
+                    size_for_dir(meta_dir(m), T.body_w, T.body_h, bw, bh);
+                    fill_area(v.cells, gp.W, (int)(p & 0xFFFF), (int)(p >> 16), bw, bh, kCellEmpty);
                     atomicAdd(&v.grp_dead[g], 1);
                 }
             }
@@ -1284,6 +1398,11 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         }
         psync<kW>();
         order = sorted;
+    }
+    if (gp.turn_mode) {                            // turns first, same bucket order (GridWorld.cc:597-624)
+        if (TID == 0)
+            for (int i = 0; i < n_mov; ++i) do_turn_one(gp, sm, v, order[i]);
+        psync<kW>();
     }
     par = par0 && (MFX_PAR_MASK & 2);
     if (kW && par) {
@@ -1426,7 +1545,7 @@ __device__ __forceinline__ void clear_dead_env(const GameParams& gp, EnvView& v,
                 v.last_r[id] = v.next_r[id];
                 v.next_r[id] = step_reward;
                 v.op_obj[id] = -1;
-                v.meta[id] = (uint8_t)meta_make(0, kOpNull, g);
+                v.meta[id] = (uint8_t)meta_keep_dir(meta_make(0, kOpNull, g), v.meta[id]);
             }
             base += tot;
             psync<kW>();
@@ -1468,6 +1587,7 @@ __global__ void __launch_bounds__(256) k_get(const GameParams* __restrict__ gp, 
             } break;
             case kGetHp: reinterpret_cast<float*>(out)[o + i] = v.hp[id]; break;
             case kGetLastAct: reinterpret_cast<int*>(out)[o + i] = v.last_act[id]; break;
+            case kGetDir: reinterpret_cast<int*>(out)[o + i] = meta_dir(v.meta[id]); break;
             default: break;
         }
     }
@@ -1511,8 +1631,8 @@ __device__ __forceinline__ int rush_action(const GameParams& gp, const SerialTyp
         int hit = -1;
 #pragma unroll
         for (int j = 7; j >= 0; --j) {
-            const uint32_t m = v.meta[c[j] < kCellWall ? c[j] : 0u];
-            if (c[j] < kCellWall && (int)meta_group(m) != g) hit = k0 + j;
+            const uint32_t m = v.meta[c[j] < kCellFood ? c[j] : 0u];
+            if (c[j] < kCellFood && (int)meta_group(m) != g) hit = k0 + j;
         }
         if (hit >= 0) { a = S.attack_base + hit; break; }
     }
@@ -2163,8 +2283,24 @@ hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st) 
 }
 
 hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
-                             const int* d_xs, const int* d_ys, int per_env_stride, hipStream_t st) {
-    k_add_agents<<<(s.E + 63) / 64, 64, 0, st>>>(d_gp, s, group, n, method, d_xs, d_ys, per_env_stride);
+                             const int* d_xs, const int* d_ys, const int* d_dirs, int per_env_stride, hipStream_t st) {
+    k_add_agents<<<(s.E + 63) / 64, 64, 0, st>>>(d_gp, s, group, n, method, d_xs, d_ys, d_dirs, per_env_stride);
+    return hipGetLastError();
+}
+
+// GridWorld::set_goal "random" (GridWorld.cc:729-740, deprecated): the goals are never read again, but
+// the two LCG draws per agent move the engine's random stream.
+__global__ void k_set_goal_random(const GameParams* __restrict__ gp, State s, int g) {
+    const int e = blockIdx.x * blockDim.x + TID;
+    if (e >= s.E) return;
+    const int n = s.grp_n[e * gp->n_groups + g];
+    uint32_t rng = s.rng[e];
+    for (int i = 0; i < 2 * n; ++i) rng = minstd_next(rng);
+    s.rng[e] = rng;
+}
+
+hipError_t launch_set_goal_random(const GameParams* d_gp, const State& s, int g, hipStream_t st) {
+    k_set_goal_random<<<(s.E + 63) / 64, 64, 0, st>>>(d_gp, s, g);
     return hipGetLastError();
 }
 

@@ -13,7 +13,7 @@
 //     last_act  u8  [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145)
 //     op_obj    i32 [E][cap]   id of Agent::op_obj or -1
 //     meta      u8  [E][cap]   bit0 dead | bits1-2 last_op | bit3 involved (reward DSL, transient)
-//                              | bits4-5 group
+//                              | bits4-5 group | bits6-7 direction ^ 3 (0 = NORTH, turn_mode)
 //   groups
 //     grp_ids   u16 [E][G][cap] the ordered agent vector of each group (Group::agents)
 //     grp_n, grp_dead i32 [E][G];  grp_reward f32 [E][G]
@@ -36,6 +36,7 @@ constexpr int kMaxSyms = 16;        // reward DSL: agent symbols, event nodes (R
 constexpr int kMaxNodes = 32;
 constexpr uint16_t kCellEmpty = 0xFFFF;
 constexpr uint16_t kCellWall = 0xFFFE;
+constexpr uint16_t kCellFood = 0xFFFD;   // food_mode: a food slot (amount in State::food); ids stay below
 constexpr uint32_t kBucketBoundary = 0xFF;
 
 // last_op encoding in meta bits 1-2
@@ -53,6 +54,8 @@ struct TypeParams {                 // AgentType (AgentType.h:17-52), the fields
     int view_w, view_h, view_x1, view_y1;      // view window relative to the agent (NORTH)
     int att_x_off, att_y_off;
     int body_w, body_h;                        // width x length cells from pos (NORTH, Map.cc:75-97)
+    int view_off_x, view_off_y, view_lt_x, view_lt_y;   // turn_mode: eye offset and window corner (rela)
+    float eat_ability, food_supply;            // food_mode (Map.cc:289-303, AgentType.h)
     int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];
     int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];
     uint8_t view_mask[kMaxViewCells];          // Range::is_in, row-major [view_h][view_w]
@@ -97,6 +100,7 @@ struct GameParams {
     int par_step;                   // 1: attack / move resolution may run in parallel (every
                                     //    kill_supply == 0, so a kill never changes the killer's hp)
     int dsl;                        // 1: reward rules outside the RuleParams form run through `prog`
+    int turn_mode, food_mode;       // GridWorld.cc:138-147 (serial / generic paths only)
     int feat_size[kMaxGroups];
     TypeParams type[kMaxGroups];    // per group (Group::type)
     RuleParams rules[kMaxRules];
@@ -124,6 +128,7 @@ struct State {                      // device pointers; every array is [E][strid
     uint32_t* mov;                  // [E][acap]
     int32_t* n_mov;                 // [E]
     int32_t* done;                  // [E]
+    float* food;                    // [E][H*W] food amount where cells == kCellFood (food_mode only)
     int32_t* idx_mark;              // [E] id_counter at the last clear_dead: Agent::index is the list
                                     //     position for ids below it, else 0 (GridWorld.h:139, :718)
     int32_t* err;                   // [1] sticky device-side error code
@@ -177,5 +182,13 @@ __host__ __device__ inline uint32_t meta_group(uint32_t m) { return (m >> 4) & 3
 __host__ __device__ inline uint32_t meta_make(uint32_t dead, uint32_t op, uint32_t g) {
     return dead | (op << 1) | (g << 4);
 }
+// Direction (grid_def.h:15): EAST 0, SOUTH 1, WEST 2, NORTH 3; stored xor 3 so that every meta
+// built without direction bits faces NORTH.
+enum : int { kDirEast = 0, kDirSouth = 1, kDirWest = 2, kDirNorth = 3 };
+__host__ __device__ inline int meta_dir(uint32_t m) { return (int)(((m >> 6) & 3u) ^ 3u); }
+__host__ __device__ inline uint32_t meta_set_dir(uint32_t m, int dir) {
+    return (m & 0x3Fu) | ((((uint32_t)dir ^ 3u) & 3u) << 6);
+}
+__host__ __device__ inline uint32_t meta_keep_dir(uint32_t fresh, uint32_t old) { return fresh | (old & 0xC0u); }
 
 }  // namespace mfx

@@ -184,3 +184,49 @@ def test_odd_bodies_fill_and_custom_placement():
         return out
 
     _compare(run(common.HIP_LIB), run(common.REF_LIB))
+
+
+def _mode_config(map_size, turn, food, minimap, goal=False, big=False):
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": map_size, "map_height": map_size, "turn_mode": turn, "food_mode": food,
+             "minimap_mode": minimap, "goal_mode": goal, "embedding_size": 6})
+    hunter = cfg.register_agent_type("hunter", dict(
+        width=2 if big else 1, length=3 if big else 1, hp=6, speed=1.5, view_range=gw.CircleRange(3),
+        attack_range=gw.CircleRange(1.5), damage=2, step_recover=0.1, eat_ability=1.5, food_supply=2.5,
+        kill_reward=3, attack_penalty=-0.1, step_reward=-0.01))
+    prey = cfg.register_agent_type("prey", dict(
+        width=1, length=1, hp=4, speed=1, view_range=gw.SectorRange(3, 120), attack_range=gw.CircleRange(1),
+        damage=1, step_recover=-0.02, eat_ability=0.4, food_supply=1.2, kill_supply=1.0, dead_penalty=-1))
+    g0, g1 = cfg.add_group(hunter), cfg.add_group(prey)
+    a, b = gw.AgentSymbol(g0, "any"), gw.AgentSymbol(g1, "any")
+    cfg.add_reward_rule(gw.Event(a, "attack", b), receiver=[a, b], value=[0.2, -0.2])
+    cfg.add_reward_rule(gw.Event(b, "collide", a), receiver=b, value=0.05)
+    return cfg
+
+
+@pytest.mark.parametrize("turn,food,minimap,big,seed", [
+    (True, False, False, False, 11), (True, False, True, True, 12), (False, True, True, False, 13),
+    (False, True, False, True, 14), (True, True, True, False, 15), (True, True, False, True, 16)])
+def test_turn_and_food_modes_match_reference(turn, food, minimap, big, seed):
+    """turn_mode (random directions from the LCG, turn actions with the reference's wise = 2a - 1,
+    direction-relative moves / attacks / views, bodies pivoting about their real corner) and
+    food_mode (a kill leaves food_supply on the hit cell, attacks eat min(eat_ability, food), food
+    blocks moves and shows on channel 1), alone and together, 1x1 and 2x3 bodies."""
+    _both(_mode_config(16, turn, food, minimap, big=big), 16, (14, 30), seed, steps=60, walls=6)
+
+
+def test_goal_mode_and_set_goal_rng():
+    """goal_mode adds two (always zero) features; set_goal('random') draws two LCG numbers per agent
+    (GridWorld.cc:729-740), which later random placements see."""
+    def run(lib_path):
+        env, (h0, h1) = common.config_env(lib_path, _mode_config(14, False, False, True, goal=True), 14)
+        env.set_seed(21)
+        env.reset()
+        env.add_agents(h0, method="random", n=6)
+        env._lib.gridworld_set_goal(env.game, 0, b"random", None)
+        env.add_agents(h1, method="random", n=9)
+        view, feat = env.get_observation(h1)
+        return [feat.copy(), view.copy(), env.get_pos(h0).copy(), env.get_pos(h1).copy()]
+    _compare([run(common.HIP_LIB)], [run(common.REF_LIB)])
