@@ -60,8 +60,14 @@ def test_engine_fails_loudly_without_gpu(built):
 
 
 def test_dropin_rejects_unsupported_config(built):
+    """can_absorb is the one agent attribute the engine refuses; the error surfaces at
+    register_agent_type, before any device work, so this runs without a GPU."""
     import magent
-    cfg = magent.gridworld.Config()
-    cfg.set({"map_width": 10, "map_height": 10, "turn_mode": True})
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": 10, "map_height": 10, "turn_mode": True, "food_mode": True})
+    cfg.register_agent_type("blob", {"width": 1, "length": 1, "hp": 1, "speed": 1, "can_absorb": True,
+                                     "view_range": gw.CircleRange(1), "attack_range": gw.CircleRange(1)})
+    cfg.add_group("blob")
     with pytest.raises(magent.EngineError):
         magent.GridWorld(cfg, lib=magent.load_library(built))
