@@ -443,7 +443,10 @@ public:
             T.eat_ability = t.eat_ability; T.food_supply = t.food_supply;
             for (int i = 0; i < t.move.count; i++) { T.move_dx[i] = (int8_t)t.move.dx[i]; T.move_dy[i] = (int8_t)t.move.dy[i]; }
             for (int i = 0; i < t.attack.count; i++) { T.att_dx[i] = (int8_t)t.attack.dx[i]; T.att_dy[i] = (int8_t)t.attack.dy[i]; }
-            for (int i = 0; i < t.view.w * t.view.h; i++) T.view_mask[i] = t.view.in[i];
+            for (int i = 0; i < t.view.w * t.view.h; i++) {
+                T.view_mask[i] = t.view.in[i];
+                if (t.view.in[i]) T.view_bits[i >> 5] |= 1u << (i & 31);
+            }
             p.feat_size[g] = feature_size(g);
         }
         // reward rules: the common form (one attack/kill/collide event between 'any' agents of two
@@ -687,7 +690,7 @@ public:
             if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return fail("rollout: 1x1 bodies only; use the per-call API");
         try {
             ensure_capacity(total, total);
-            const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+            const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rowcap);
             if (smem > 160 * 1024)
                 return fail("rollout: env does not fit in LDS (%zu bytes); use the per-call API", smem);
             std::vector<int> hx((size_t)G * tcap, 0), hy((size_t)G * tcap, 0);
@@ -750,7 +753,7 @@ public:
             ra.work = ro_work.p; ra.work_sel = 0; ra.reset_image = ro_image.p;
             ra.cls_cnt = ro_cls_cnt.p; ra.cls_list = ro_cls_list.p; ra.cls_stride = E;
             MFX_HIP_THROW(launch_reset_image(gp, d_gp, s, ra, ro_image.p, stream));
-            MFX_HIP_THROW(rollout_grid(gp, s, &ro_grid));
+            MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, &ro_grid));
             ro_cap = s.cap;
             ro_ctx.ensure(1);
             ro_ctx_host.s = s; ro_ctx_host.ra = ra;
@@ -766,8 +769,8 @@ public:
         if (!rollout_ready) return fail("rollout_step before rollout_init");
         if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
         for (int i = 0; i < n_steps; i++) {
-            MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.step_index, ra.work_sel, (int)(ro_launch % 6), ro_grid,
-                                   stream));
+            MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
+                                   ro_grid, stream));
             ro_launch++;
             ra.step_index++;
             ra.work_sel ^= 1;
@@ -778,7 +781,7 @@ public:
     int rollout_info(int* grid, int* lds_bytes) {
         if (!rollout_ready) return fail("rollout_info before rollout_init");
         *grid = ro_grid;
-        *lds_bytes = (int)rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+        *lds_bytes = (int)rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, ra.rowcap);
         return 0;
     }
 

@@ -23,10 +23,10 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
                        uint32_t* d_sort_scratch, hipStream_t st);
 hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st);
 hipError_t set_stamp_buffer(unsigned long long* d_buf);
-size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap);
+size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap, int rows);
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                          uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st);
-hipError_t rollout_grid(const GameParams& gp, const State& s, int* grid);
+                          int rows, uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st);
+hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int* grid);
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap);
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
                               uint4* d_image, hipStream_t st);

@@ -283,12 +283,12 @@ struct ObsSmem {                  // LDS carve-up of the observation kernels
     float* stage;                 // [kObsK][VH*VW*n_ch]
     float* mm;                    // [G][VH*VW] minimap density
     int* hist;                    // [G][VH*VW]
-    uint16_t* bin;                // [cap] minimap cell of every agent id (this call)
-    uint8_t* mask;                // [VH*VW]
+    uint16_t* bin;                // [cap] minimap cell of every agent id (generic path only)
+    uint32_t* mask;               // [ceil(VH*VW/32)] view mask bits (Range::is_in)
     float* type_hp;               // [G]
     uint32_t* info;               // [cap] wave-streamed path: hp / max hp bits | group << 31, or null
-    uint2* aq;                    // [cap] wave-streamed path: per agent of the group being observed,
-                                  //       view origin (int16 x | int16 y << 16) and minimap bin
+    uint32_t* aq;                 // [rows] wave-streamed path: per agent of the group being observed,
+                                  //       view origin + 8 (12 bits x, 12 bits y) | minimap bin << 24
 };
 
 // Battle fast path (builtin/config/battle.py): 13x13 view, 7 channels, 2 groups, minimap, 34
@@ -311,7 +311,7 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
             const int id = v.grp_ids[j * v.cap + i];
             const uint32_t p = v.xy[id];
             const int b = ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw;
-            sm.bin[id] = (uint16_t)b;
+            if (!kB) sm.bin[id] = (uint16_t)b;
             atomicAdd(&sm.hist[j * NV + b], 1);
             // hp / max hp (Map.cc:208), once per agent instead of once per viewer; the group rides
             // in the sign bit (a visible agent's hp is >= +0)
@@ -361,7 +361,7 @@ __device__ __forceinline__ void obs_rows(const GameParams& gp, const EnvView& v,
             rela_to_abs(rx, ry, dir, T.view_off_x, T.view_off_y, ex, ey);
             rela_to_abs(ex, ey, dir, T.view_lt_x + vx, T.view_lt_y + vy, mx, my);
         }
-        if (sm.mask[c] && mx >= 0 && my >= 0 && mx < W && my < H) {
+        if (((sm.mask[c >> 5] >> (c & 31)) & 1u) && mx >= 0 && my >= 0 && mx < W && my < H) {
             const uint32_t cv = v.cells[my * W + mx];
             if (cv == kCellWall) {
                 o[0] = 1.0f;
@@ -438,11 +438,15 @@ __device__ __forceinline__ void obs_agent_records(const GameParams& gp, const En
                                                   int n) {
     const TypeParams& T = gp.type[g];
     const uint16_t* ids = v.grp_ids + g * v.cap;
+    constexpr int VW = BattleShape::VW, VH = BattleShape::VH;
+    const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;   // obs_minimap's scale
     for (int a = TID; a < n; a += blockDim.x) {
         const int id = ids[a];
         const uint32_t p = v.xy[id];
-        const int ox = (int)(p & 0xFFFF) + T.view_x1, oy = (int)(p >> 16) + T.view_y1;
-        sm.aq[a] = make_uint2(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16), sm.bin[id]);
+        const int x = (int)(p & 0xFFFF), y = (int)(p >> 16);
+        const int ox = x + T.view_x1 + 8, oy = y + T.view_y1 + 8;        // >= 2, < 4096 (is_battle_shape)
+        const int b = (y / sh) * VW + x / sw;
+        sm.aq[a] = (uint32_t)ox | ((uint32_t)oy << 12) | ((uint32_t)b << 24);
     }
 }
 
@@ -460,11 +464,11 @@ __device__ __forceinline__ CellObs obs_cell(const EnvView& v, const ObsSmem& sm,
     const int gs = valid ? gc : 0;
     const int a = gs / NV, c = gs - a * NV;
     const int vy = c / BattleShape::VW, vx = c - vy * BattleShape::VW;
-    const uint2 q = sm.aq[a];
-    const uint32_t mk = sm.mask[c];
+    const uint32_t q = sm.aq[a];
+    const uint32_t mk = (sm.mask[c >> 5] >> (c & 31)) & 1u;
     const float mo = mm_own[c], me = mm_en[c];
-    const bool self = c == (int)q.y;
-    const int mx = (int)(int16_t)(q.x & 0xFFFFu) + vx, my = ((int)q.x >> 16) + vy;
+    const bool self = c == (int)(q >> 24);
+    const int mx = (int)(q & 0xFFFu) - 8 + vx, my = (int)((q >> 12) & 0xFFFu) - 8 + vy;
     const bool ok = valid && mk != 0 && (unsigned)mx < (unsigned)W && (unsigned)my < (unsigned)H;
     const uint32_t cv = v.cells[ok ? my * W + mx : 0];
     const bool agent = ok && cv < kCellFood;
@@ -582,6 +586,7 @@ __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const En
 __host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
     if (gp.n_groups != BattleShape::G || !gp.minimap || gp.n_ch != BattleShape::NC || gp.turn_mode || gp.food_mode)
         return false;
+    if (gp.W > 4000 || gp.H > 4000) return false;                // packed view origins (obs_agent_records)
     for (int g = 0; g < gp.n_groups; ++g) {
         if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return false;
         if (gp.type[g].view_w != BattleShape::VW || gp.type[g].view_h != BattleShape::VH ||
@@ -596,15 +601,18 @@ __host__ __device__ inline bool is_battle_shape(const GameParams& gp) {
 
 // LDS of the observation phase.  stage_floats: the staging area (K rows for the staged path,
 // one 448-float slice per wave for the wave-streamed path).
-__host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int cap, size_t stage_floats) {
+// rows: agents of one group observed per call (records of the wave-streamed path); kB: Battle path
+// (no per-id minimap bins).
+__host__ __device__ inline size_t obs_smem_core(const GameParams& gp, int g, int cap, int rows, size_t stage_floats,
+                                                bool kB) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t NV = (size_t)gp.type[g].view_w * gp.type[g].view_h;
-    return r16(stage_floats * 4) + r16((size_t)gp.n_groups * NV * 4) + r16((size_t)cap * 2) + 16 + r16(NV) +
-           r16((size_t)cap * 4) + r16((size_t)cap * 8);
+    return r16(stage_floats * 4) + r16((size_t)gp.n_groups * NV * 4) + (kB ? 0 : r16((size_t)cap * 2)) + 16 +
+           r16((NV + 31) / 32 * 4) + r16((size_t)cap * 4) + r16((size_t)rows * 4);
 }
 
-__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, int cap, size_t stage_floats,
-                                             size_t& off) {
+__device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, int g, int cap, int rows,
+                                             size_t stage_floats, bool kB, size_t& off) {
     const TypeParams& T = gp.type[g];
     const size_t NV = (size_t)T.view_w * T.view_h, G = gp.n_groups;
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -612,11 +620,11 @@ __device__ __forceinline__ ObsSmem carve_obs(char* smem, const GameParams& gp, i
     sm.stage = reinterpret_cast<float*>(smem + off); off += r16(stage_floats * 4);
     sm.mm = reinterpret_cast<float*>(smem + off);    // the histogram is converted in place
     sm.hist = reinterpret_cast<int*>(smem + off);    off += r16(G * NV * 4);
-    sm.bin = reinterpret_cast<uint16_t*>(smem + off); off += r16((size_t)cap * 2);
+    sm.bin = kB ? nullptr : reinterpret_cast<uint16_t*>(smem + off); off += kB ? 0 : r16((size_t)cap * 2);
     sm.type_hp = reinterpret_cast<float*>(smem + off); off += 16;
-    sm.mask = reinterpret_cast<uint8_t*>(smem + off); off += r16(NV);
+    sm.mask = reinterpret_cast<uint32_t*>(smem + off); off += r16((NV + 31) / 32 * 4);
     sm.info = reinterpret_cast<uint32_t*>(smem + off); off += r16((size_t)cap * 4);
-    sm.aq = reinterpret_cast<uint2*>(smem + off);     off += r16((size_t)cap * 8);
+    sm.aq = reinterpret_cast<uint32_t*>(smem + off);  off += r16((size_t)rows * 4);
     return sm;
 }
 
@@ -628,7 +636,7 @@ __host__ __device__ inline size_t obs_stage_floats(const GameParams& gp, int g, 
 __device__ __forceinline__ void obs_prologue(const GameParams& gp, const ObsSmem& sm, int g) {
     const TypeParams& T = gp.type[g];
     const int NV = T.view_w * T.view_h;
-    for (int i = TID; i < NV; i += blockDim.x) sm.mask[i] = T.view_mask[i];
+    for (int w = TID; w < (NV + 31) / 32; w += blockDim.x) sm.mask[w] = T.view_bits[w];
     if (TID < gp.n_groups) sm.type_hp[TID] = gp.type[TID].hp;
 }
 
@@ -648,7 +656,7 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     const int a_end = min(n, a_begin + chunk);
     if (a_end > rowcap) { if (TID == 0) set_err(s, 4); return; }
     size_t off = 0;
-    ObsSmem sm = carve_obs(smem, gp, g, s.cap, obs_stage_floats(gp, g, kB, blockDim.x), off);
+    ObsSmem sm = carve_obs(smem, gp, g, s.cap, chunk, obs_stage_floats(gp, g, kB, blockDim.x), kB, off);
     if (!kB) sm.info = nullptr;
     if (cells_in_lds) {
         uint16_t* lc = reinterpret_cast<uint16_t*>(smem + off);
@@ -743,6 +751,11 @@ struct StepSmem {
     int flags[8];       // [0..kMaxRules) rule triggers
     SerialType tt[kMaxGroups];
 };
+
+// StepSmem lives in dynamic LDS with room for the env's G type entries only.
+__host__ __device__ inline size_t step_sm_bytes(int G) {
+    return ((offsetof(StepSmem, tt) + (size_t)G * sizeof(SerialType)) + 15) & ~(size_t)15;
+}
 
 __device__ __forceinline__ void load_serial_types(const GameParams& gp, StepSmem& sm) {
     for (int g = 0; g < gp.n_groups; ++g) {
@@ -1469,9 +1482,9 @@ template <bool kDsl>
 __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp, State s, int lds,
                                               uint32_t* __restrict__ sort_scratch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ StepSmem sm;
     const GameParams& gp = *gpp;
     const int e = blockIdx.x, G = gp.n_groups;
+    StepSmem& sm = *reinterpret_cast<StepSmem*>(smem);
     EnvView gv = global_view(s, e, G);
     EnvView v = gv;
     const int nid = s.id_counter[e];
@@ -1480,7 +1493,7 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     uint32_t* mov = s.mov + (size_t)e * s.acap;
     uint32_t* sorted = sort_scratch + (size_t)e * s.acap;
     if (lds) {
-        size_t off = 0;
+        size_t off = step_sm_bytes(G);
         auto carve = [&](size_t bytes) { char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
         v.cells = reinterpret_cast<uint16_t*>(carve((size_t)s.cells_n * 2));
         v.xy = reinterpret_cast<uint32_t*>(carve((size_t)nid * 4));
@@ -1679,8 +1692,9 @@ __host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int 
     return u;
 }
 
-__host__ __device__ inline size_t rollout_scratch_bytes(const GameParams& gp, int cap, int acap, int threads) {
-    const size_t obs = obs_smem_core(gp, 0, cap, obs_stage_floats(gp, 0, is_battle_shape(gp), threads));
+__host__ __device__ inline size_t rollout_scratch_bytes(const GameParams& gp, int cap, int acap, int rows, int threads,
+                                                        bool kB) {
+    const size_t obs = obs_smem_core(gp, 0, cap, rows, obs_stage_floats(gp, 0, kB, threads), kB);
     const size_t stp = rollout_union(gp, cap, acap, threads).total;
     return obs > stp ? obs : stp;
 }
@@ -1692,8 +1706,19 @@ __host__ __device__ inline size_t env_image_bytes(int cells_n, int cap, int G) {
     return r16((size_t)cells_n * 2) + 5 * r16((size_t)cap * 4) + 2 * r16(cap) + r16((size_t)G * cap * 2);
 }
 
-size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap) {
-    return env_image_bytes(cells_n, cap, gp.n_groups) + rollout_scratch_bytes(gp, cap, acap, MFX_ROLLOUT_THREADS);
+#ifndef MFX_LDS_PAD
+#define MFX_LDS_PAD 0              // experiments only: extra dynamic LDS per workgroup (lowers occupancy)
+#endif
+// env image | scratch union | StepSmem (G type entries)
+__host__ __device__ inline size_t rollout_main_bytes(const GameParams& gp, int cells_n, int cap, int acap, int rows,
+                                                     bool kB) {
+    return env_image_bytes(cells_n, cap, gp.n_groups) +
+           rollout_scratch_bytes(gp, cap, acap, rows, MFX_ROLLOUT_THREADS, kB);
+}
+
+size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap, int rows) {
+    return rollout_main_bytes(gp, cells_n, cap, acap, rows, is_battle_shape(gp)) + step_sm_bytes(gp.n_groups) +
+           MFX_LDS_PAD;
 }
 
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap) {
@@ -2057,7 +2082,6 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
                                                                  const RolloutCtx* __restrict__ ctx,
                                                                  uint32_t step_index, int work_sel, int qphase) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ StepSmem sm;
     __shared__ EnvScalars sc;
     __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 3 episode end, 4 done, 5-7 queue hand-off
     __shared__ int32_t n_before[kMaxGroups];
@@ -2066,6 +2090,10 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
     __shared__ int wg_env[kQueueBuf];
     __shared__ uint8_t wg_cls[kQueueBuf];
     __shared__ int wg_n;                     // envs buffered in wg_env / wg_cls
+    // StepSmem (serial type table, scan / flag words) follows the env image and the scratch union
+    StepSmem& sm = *reinterpret_cast<StepSmem*>(
+        smem + rollout_main_bytes(kconst(gpp), kconst(ctx).s.cells_n, kconst(ctx).s.cap, kconst(ctx).s.acap,
+                                  kconst(ctx).ra.rowcap, kB));
     // Work queue: position i of this launch is env queue_env(i) (class lists, heaviest first).
     // The hand-off is pipelined so that no queue access is waited on: while env e_k is processed,
     // e_{k+1} is being prefetched, thread 0 holds e_{k+2} (o) and the queue slot of e_{k+3} (g),
@@ -2117,7 +2145,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
     const size_t soff = env_image_bytes(s.cells_n, cap, G);
     char* uni = smem + soff;                 // scratch shared by the observation and the step phases
     size_t soff2 = soff;
-    ObsSmem osm = carve_obs(smem, gp, 0, cap, obs_stage_floats(gp, 0, kB, blockDim.x), soff2);
+    ObsSmem osm = carve_obs(smem, gp, 0, cap, ra.rowcap, obs_stage_floats(gp, 0, kB, blockDim.x), kB, soff2);
     if (!kB) osm.info = nullptr;
     const RolloutUnion u = rollout_union(gp, cap, acap, blockDim.x);
     int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
@@ -2266,7 +2294,8 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
 //  host-side launchers
 // ==================================================================================
 size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n, int cap) {
-    size_t b = obs_smem_core(gp, g, cap, obs_stage_floats(gp, g, is_battle_shape(gp), 256));
+    const bool kB = is_battle_shape(gp);
+    size_t b = obs_smem_core(gp, g, cap, 64, obs_stage_floats(gp, g, kB, 256), kB);
     if (cells_in_lds) b += (size_t)cells_n * 2;
     return b;
 }
@@ -2327,10 +2356,11 @@ hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, cons
 
 hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State& s, int max_ids,
                        uint32_t* d_sort_scratch, hipStream_t st) {
-    const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap);
+    const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap) + step_sm_bytes(gp.n_groups);
     const int lds = smem <= 96 * 1024;
-    if (gp.dsl) k_step<true><<<s.E, 256, lds ? smem : 0, st>>>(d_gp, s, lds, d_sort_scratch);
-    else k_step<false><<<s.E, 256, lds ? smem : 0, st>>>(d_gp, s, lds, d_sort_scratch);
+    const size_t dyn = lds ? smem : step_sm_bytes(gp.n_groups);
+    if (gp.dsl) k_step<true><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+    else k_step<false><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
     return hipGetLastError();
 }
 
@@ -2364,8 +2394,8 @@ static hipError_t with_rollout_kernel(const GameParams& gp, const State& s, F&& 
 }
 
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                          uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st) {
-    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+                          int rows, uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st) {
+    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rows);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     return with_rollout_kernel(gp, s, [&](auto kern) {
         kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel, qphase);
@@ -2375,8 +2405,8 @@ hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const St
 
 // Persistent grid of k_rollout: every workgroup that can be resident at once (more is harmless --
 // the extra ones find the queue empty -- fewer would idle CUs).
-hipError_t rollout_grid(const GameParams& gp, const State& s, int* grid) {
-    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap);
+hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int* grid) {
+    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rows);
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t err = hipGetDevice(&dev);
     if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -59,6 +59,7 @@ struct TypeParams {                 // AgentType (AgentType.h:17-52), the fields
     int8_t move_dx[kMaxRangeCount], move_dy[kMaxRangeCount];
     int8_t att_dx[kMaxRangeCount], att_dy[kMaxRangeCount];
     uint8_t view_mask[kMaxViewCells];          // Range::is_in, row-major [view_h][view_w]
+    uint32_t view_bits[kMaxViewCells / 32];    // the same mask, one bit per cell
 };
 
 struct RuleParams {                 // RewardRule on one binary event between two 'any' symbols
