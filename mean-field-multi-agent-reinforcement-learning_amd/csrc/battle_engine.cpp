@@ -144,6 +144,9 @@ public:
     DevBuf<int32_t> ro_cls_cnt, ro_cls_list; // k_rollout work queue (weight-class lists)
     uint64_t ro_launch = 0;                  // launches so far (queue phase = ro_launch % 6)
     DevBuf<uint4> ro_image;                  // reset image (k_reset_image)
+    DevBuf<uint4> ro_walls;                  // its cells without the agents (RolloutArgs::wall_image)
+    bool cells_stale = false;                // State::cells lags the fused rollout (sync_cells)
+    bool walls_after_init = false;           // walls added after rollout_init: not in the rollout's cells
     DevBuf<RolloutCtx> ro_ctx;               // device copy of {s, ra} read by k_rollout
     RolloutCtx ro_ctx_host{};
     int ro_grid = 0, ro_cap = 0;
@@ -554,6 +557,7 @@ public:
             if (food && !s.food) alloc(s.food, (size_t)E * W * H);
             MFX_HIP_THROW(hipMemcpyAsync(d_gp, &gp, sizeof(GameParams), hipMemcpyHostToDevice, stream));
             MFX_HIP_THROW(launch_reset(d_gp, s, stream));
+            cells_stale = false;
             next_file();                              // GridWorld.cc:102
             max_ids = 0;
             std::fill(group_ub.begin(), group_ub.end(), 0);
@@ -568,6 +572,8 @@ public:
     int add_agents(int group, int n, const char* method, const int* xs, const int* ys, const int* dirs) {
         if (!allocated) return fail("add_agents before reset");
         if (group >= n_groups() || group < -1) return fail("invalid group handle in add_agents: %d", group);
+        MFX_CHECK(sync_cells());
+        if (group < 0 && rollout_ready) walls_after_init = true;
         int m, count;
         std::vector<int> hx, hy, hd;
         if (!strcmp(method, "custom")) {
@@ -639,8 +645,18 @@ public:
     }
 
     // ------------------------------------------------------------------ batched device API
+    // The fused rollout keeps the cells in LDS only; rebuild State::cells before the per-call path
+    // (or anything else that reads them) runs after rollout steps.
+    int sync_cells() {
+        if (!cells_stale) return 0;
+        MFX_HIP(launch_rebuild_cells(d_gp, s, ro_walls.p, stream));
+        cells_stale = false;
+        return 0;
+    }
+
     int observe(int g, float* d_view, float* d_feat, int rowcap) {
         if (!allocated || g < 0 || g >= n_groups()) return fail("observe: bad state or group");
+        MFX_CHECK(sync_cells());
         MFX_HIP(launch_observe(gp, d_gp, s, g, group_ub[g], d_view, d_feat, rowcap, stream));
         return 0;
     }
@@ -653,6 +669,7 @@ public:
     }
     int step(int* d_done) {
         if (!allocated) return fail("step before reset");
+        MFX_CHECK(sync_cells());
         MFX_HIP(launch_step(gp, d_gp, s, max_ids, d_sort, stream));
         pending_ub = 0;
         if (d_done) MFX_HIP(hipMemcpyAsync(d_done, s.done, sizeof(int32_t) * E, hipMemcpyDeviceToDevice, stream));
@@ -732,6 +749,7 @@ public:
         for (int g = 0; g < G; g++) MFX_CHECK(add_agents(g, tmpl_n[g], "custom", xs[g], ys[g], nullptr));
         MFX_CHECK(rollout_plan());
         rollout_ready = true;
+        walls_after_init = false;
         return 0;
     }
 
@@ -753,6 +771,15 @@ public:
             ra.work = ro_work.p; ra.work_sel = 0; ra.reset_image = ro_image.p;
             ra.cls_cnt = ro_cls_cnt.p; ra.cls_list = ro_cls_list.p; ra.cls_stride = E;
             MFX_HIP_THROW(launch_reset_image(gp, d_gp, s, ra, ro_image.p, stream));
+            {   // the walls of the reset image (agents removed), shared by every env's install
+                std::vector<uint16_t> cells((size_t)s.cells_n);
+                MFX_HIP_THROW(hipStreamSynchronize(stream));
+                MFX_HIP_THROW(hipMemcpy(cells.data(), ro_image.p, cells.size() * 2, hipMemcpyDeviceToHost));
+                for (auto& c : cells) if (c < kCellFood) c = kCellEmpty;
+                ro_walls.ensure((cells.size() * 2 + 15) / 16);
+                MFX_HIP_THROW(hipMemcpy(ro_walls.p, cells.data(), cells.size() * 2, hipMemcpyHostToDevice));
+                ra.wall_image = ro_walls.p;
+            }
             MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, &ro_grid));
             ro_cap = s.cap;
             ro_ctx.ensure(1);
@@ -767,6 +794,7 @@ public:
 
     int rollout_step(int n_steps) {
         if (!rollout_ready) return fail("rollout_step before rollout_init");
+        if (walls_after_init) return fail("rollout: walls added after rollout_init are not part of the rollout's episodes");
         if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
         for (int i = 0; i < n_steps; i++) {
             MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
@@ -774,6 +802,7 @@ public:
             ro_launch++;
             ra.step_index++;
             ra.work_sel ^= 1;
+            cells_stale = n_steps > 0;
         }
         return 0;
     }
@@ -1017,6 +1046,7 @@ public:
 
     // Keys the python wrapper asks with group -1 (gridworld.py:526-636).
     int get_info_global(int group, const char* name, void* buf) {
+        MFX_CHECK(sync_cells());
         int* ib = (int*)buf;
         float* fb = (float*)buf;
         const int G = n_groups();

@@ -15,6 +15,7 @@ hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st);
 hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
                              const int* d_xs, const int* d_ys, const int* d_dirs, int per_env_stride, hipStream_t st);
 hipError_t launch_set_goal_random(const GameParams* d_gp, const State& s, int g, hipStream_t st);
+hipError_t launch_rebuild_cells(const GameParams* d_gp, const State& s, const void* walls, hipStream_t st);
 hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
                           float* d_view, float* d_feat, int rowcap, hipStream_t st);
 hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, const int* d_actions, int rowcap,

@@ -1831,6 +1831,7 @@ struct EnvPrefetch {
 // separate pointers per lane instead would serialise the loads (each predicated load into the same
 // registers waits for the previous one).
 struct PfTable {
+    unsigned long long walls;           // RolloutArgs::wall_image (cells rows, shared by every env)
     unsigned long long base[8];         // xy hp next_r last_r op_obj, last_act, meta, grp_ids
     unsigned int stride[8];
     unsigned long long sbase[32];       // 0: word absent (group >= G, padding)
@@ -1840,6 +1841,7 @@ struct PfTable {
 __device__ __forceinline__ void pf_table_init(PfTable& pt, const State& s, const RolloutArgs& ra, int G) {
     const int t = TID;
     const unsigned cap4 = (unsigned)s.cap * 4u;
+    if (t == 0) pt.walls = (unsigned long long)ra.wall_image;
     if (t < 8) {
         const void* p = nullptr;
         unsigned st = cap4;
@@ -1902,7 +1904,7 @@ __device__ __forceinline__ const g_u32x4* small_row_addr(const PfTable& pt, int 
 // Address of row r of env e's whole image: the cells first, then the small part.
 __device__ __forceinline__ const g_u32x4* image_row_addr(const PfTable& pt, const State& s, int e, int r, int nc16,
                                                          int sh, int c4) {
-    const unsigned long long cells = (unsigned long long)(s.cells + (size_t)e * s.cells_n) + (unsigned)r * 16u;
+    const unsigned long long cells = pt.walls + (unsigned)r * 16u;            // walls only (L2-resident)
     return r < nc16 ? (const g_u32x4*)cells : small_row_addr(pt, e, r - nc16, sh, c4);
 }
 
@@ -1963,10 +1965,11 @@ __device__ __forceinline__ void install_sync(const State& s, const PfTable& pt, 
                                              EnvScalars& sc) {
     const EnvView gv = global_view(s, e, G);
     const int cap = s.cap;
+    const uint16_t* walls = reinterpret_cast<const uint16_t*>(pt.walls);
     if ((s.cells_n & 7) == 0) {
-        copy16(v.cells, gv.cells, (size_t)s.cells_n * 2);
+        copy16(v.cells, walls, (size_t)s.cells_n * 2);
     } else {
-        for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
+        for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = walls[i];
     }
     copy16(v.xy, gv.xy, (size_t)cap * 4);
     copy16(v.hp, gv.hp, (size_t)cap * 4);
@@ -2167,6 +2170,17 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         else install_sync(s, pt, e, G, v, sc);
         if (TID == 0) { misc[0] = 0; misc[1] = 0; misc[5] = o; }
         __syncthreads();
+        // the agents onto the walls-only cells: every listed agent is alive at an install (the lists
+        // were compacted at the end of the env's previous step)
+        for (int q = 0; q < G; ++q) {
+            const int nq = sc.grp_n[q];
+            for (int i = TID; i < nq; i += blockDim.x) {
+                const int id = v.grp_ids[q * cap + i];
+                const uint32_t p = v.xy[id];
+                if (!meta_dead(v.meta[id])) v.cells[(p >> 16) * gp.W + (p & 0xFFFF)] = (uint16_t)id;
+            }
+        }
+        __syncthreads();
         MFX_STAMP(13);
         if (TID < G) n_before[TID] = sc.grp_n[TID];
         if (kPf && en < s.E) pf_issue(pf, pt, s, en, nrows, nc16, sh, c4);
@@ -2258,12 +2272,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         // ---------------- write the env back (wave kWbWave only, see EnvPrefetch)
         if ((TID >> 6) == kWbWave) {
             const int lane = TID & 63;
-            const EnvView gv = global_view(s, e, G);
-            if ((s.cells_n & 7) == 0) {
-                wcopy16(gv.cells, v.cells, (size_t)s.cells_n * 2, lane);
-            } else {
-                for (int i = lane; i < s.cells_n; i += 64) gv.cells[i] = v.cells[i];
-            }
+            const EnvView gv = global_view(s, e, G);   // cells: rebuilt at the next install
             const int idc = sc.id_counter;
             const size_t n4 = ((size_t)idc + 3) & ~(size_t)3, n16 = ((size_t)idc + 15) & ~(size_t)15;
             wcopy16(gv.xy, v.xy, n4 * 4, lane);
@@ -2314,6 +2323,26 @@ hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st) 
 hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
                              const int* d_xs, const int* d_ys, const int* d_dirs, int per_env_stride, hipStream_t st) {
     k_add_agents<<<(s.E + 63) / 64, 64, 0, st>>>(d_gp, s, group, n, method, d_xs, d_ys, d_dirs, per_env_stride);
+    return hipGetLastError();
+}
+
+// State::cells after fused rollout steps: the walls-only image plus every live listed agent.
+__global__ void __launch_bounds__(256) k_rebuild_cells(const GameParams* __restrict__ gp, State s,
+                                                       const uint16_t* __restrict__ walls) {
+    const int e = blockIdx.x, G = gp->n_groups, W = gp->W;
+    EnvView v = global_view(s, e, G);
+    for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = walls[i];
+    __syncthreads();
+    for (int g = 0; g < G; ++g)
+        for (int i = TID; i < v.grp_n[g]; i += blockDim.x) {
+            const int id = v.grp_ids[g * s.cap + i];
+            const uint32_t p = v.xy[id];
+            if (!meta_dead(v.meta[id])) v.cells[(p >> 16) * W + (p & 0xFFFF)] = (uint16_t)id;
+        }
+}
+
+hipError_t launch_rebuild_cells(const GameParams* d_gp, const State& s, const void* walls, hipStream_t st) {
+    k_rebuild_cells<<<s.E, 256, 0, st>>>(d_gp, s, reinterpret_cast<const uint16_t*>(walls));
     return hipGetLastError();
 }
 

@@ -167,6 +167,10 @@ struct RolloutArgs {
     int work_sel;                   //     and zeroes the other one for launch k + 1
     const uint4* reset_image;       // LDS image of the env right after reset + template placement,
                                     // followed by int32 [grp_n[kMaxGroups], id_counter]
+    const uint4* wall_image;        // [H*W] u16 cells of that image with the agents removed: every
+                                    // install rebuilds the cells from it plus the agents' positions, so
+                                    // per-env cells are neither read nor written back (State::cells is
+                                    // rebuilt on demand, BattleEngine::sync_cells)
 };
 
 // Everything k_rollout reads besides GameParams, resident in HBM (uploaded when it changes); the
