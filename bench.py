@@ -35,16 +35,21 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=16384, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 16384 at 64x64, 256 at 256x256)")
+    ap.add_argument("--map", type=int, default=MAP, help="map side (64: the metric's config; 256: configs[4])")
+    ap.add_argument("--agents", type=int, default=2 * N_SIDE, help="agents per env, half per group")
     ap.add_argument("--max-steps", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.envs is None:
+        a.envs = 16384 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
+    return a
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, map_size=MAP, n_side=N_SIDE):
     """Reference engine (oracle/_ref) if built, else the C oracle, single thread, same workload.
 
     Only env calls are timed (get_observation, get_agent_id, set_action, step, get_reward,
@@ -55,10 +60,10 @@ def cpu_baseline(seconds):
     ref = os.path.join(REPO, "oracle", "_ref", "libmagent_ref.so")
     port = os.path.join(REPO, "oracle", "build", "libbattle_oracle.so")
     path, kind = (ref, "reference") if os.path.exists(ref) else (port, "port")
-    env = magent.GridWorld("battle", map_size=MAP, lib=magent.load_library(path))
+    env = magent.GridWorld("battle", map_size=map_size, lib=magent.load_library(path))
     h = env.get_handles()
     _, v2a = env.get_view2attack(h[0])
-    left, right = bd.block_positions(MAP, N_SIDE)
+    left, right = bd.block_positions(map_size, n_side)
     rng = np.random.RandomState(0)
     clock, agent_steps, episodes = 0.0, 0, 0
     while clock < seconds:
@@ -88,14 +93,16 @@ def cpu_baseline(seconds):
             k += 1
         episodes += 1
     return {"value": agent_steps / clock, "unit": "agent-steps/s", "cores": 1, "kind": kind,
-            "sample": "%d agent-steps (%d episode starts) of Battle 64x64/256 on 1 thread (OMP_NUM_THREADS=1), "
-                      "%.1f s of timed env calls; %s" % (agent_steps, episodes, clock, os.path.basename(path))}
+            "sample": "%d agent-steps (%d episode starts) of Battle %dx%d/%d on 1 thread (OMP_NUM_THREADS=1), "
+                      "%.1f s of timed env calls; %s" % (agent_steps, episodes, map_size, map_size, 2 * n_side, clock,
+                                                         os.path.basename(path))}
 
 
-def run_cpu_baseline_subprocess(seconds):
+def run_cpu_baseline_subprocess(seconds, map_size, agents):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only",
-                          "--cpu-seconds", str(seconds)], env=env, capture_output=True, text=True, timeout=600)
+                          "--cpu-seconds", str(seconds), "--map", str(map_size), "--agents", str(agents)],
+                         env=env, capture_output=True, text=True, timeout=600)
     if out.returncode != 0:
         sys.stderr.write(out.stderr)
         return None
@@ -106,7 +113,7 @@ def run_cpu_baseline_subprocess(seconds):
 def main():
     args = parse()
     if args.cpu_baseline_only:
-        print(json.dumps(cpu_baseline(args.cpu_seconds)))
+        print(json.dumps(cpu_baseline(args.cpu_seconds, args.map, args.agents // 2)))
         return
     import torch
     import torch.distributed as dist
@@ -121,11 +128,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     stream = torch.cuda.current_stream()
 
-    eng = BattleBatch(MAP, args.envs, stream=stream)
-    left, right = bd.block_positions(MAP, N_SIDE)
+    eng = BattleBatch(args.map, args.envs, stream=stream)
+    left, right = bd.block_positions(args.map, args.agents // 2)
     from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     E = args.envs
+    grid, _ = eng.rollout_info()
+    big = grid == E and args.map * args.map > 64 * 64     # k_observe + k_rollout_big (state in HBM)
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")
 
@@ -166,14 +175,14 @@ def main():
         units_per_launch = local_units / args.steps
         achieved = BYTES_PER_AGENT_STEP * units_per_launch / (kernel_ms * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "pmc_k_rollout.json")
+        pmc = os.path.join(REPO, "profiles", "pmc_big256.json" if big else "pmc_k_rollout.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("envs") == E:
-                traffic = pm.get("hbm_bytes_per_launch")
+            if pm.get("envs") == E and pm.get("map", MAP) == args.map:
+                traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_step"))
         line = {
-            "metric": "agent-steps/sec (env.step+obs) Battle 64x64x256 agents",
+            "metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents" % (args.map, args.map, args.agents),
             "value": total_units / elapsed,
             "unit": "agent-steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -183,17 +192,19 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (fixed-seed two-block placement, on-device rush policy)",
-            "config": {"workload": "Battle 64x64, 128+128 agents, %d envs per GPU, episode cap %d, fused step"
-                       % (E, args.max_steps), "map": MAP, "agents": 2 * N_SIDE, "envs_per_gpu": E,
+            "config": {"workload": "Battle %dx%d, %d+%d agents, %d envs per GPU, episode cap %d, %s"
+                       % (args.map, args.map, args.agents // 2, args.agents // 2, E, args.max_steps,
+                          "k_observe_items + k_rollout_big on 2 streams" if big else "fused step"),
+                       "map": args.map, "agents": args.agents, "envs_per_gpu": E,
                        "parallelism": "envs sharded one process per GPU (dp%d)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout", "kernel_ms": kernel_ms,
+                         "kernel": "k_observe_items+k_rollout_big" if big else "k_rollout", "kernel_ms": kernel_ms,
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = run_cpu_baseline_subprocess(args.cpu_seconds)
+            line["cpu_baseline"] = run_cpu_baseline_subprocess(args.cpu_seconds, args.map, args.agents)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

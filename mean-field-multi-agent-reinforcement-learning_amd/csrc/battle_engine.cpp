@@ -135,8 +135,16 @@ public:
     DevBuf<uint8_t> st_u8;
     // fused rollout (bench / throughput path)
     bool rollout_ready = false;
+    bool ro_big = false;                     // large envs: k_observe + k_rollout_big, state in HBM
     RolloutArgs ra{};
     DevBuf<float> ro_view[kMaxGroups], ro_feat[kMaxGroups], ro_rewards, ro_return;
+    DevBuf<float> ro_mm;                     // large envs: next observation's minimap   [E][G][169]
+    DevBuf<uint32_t> ro_info;                //             and per-id hp/max | group     [E][cap]
+    DevBuf<uint32_t> ro_sort;                //             band-ordered moves            [E][acap]
+    DevBuf<uint32_t> ro_items;               //             observation work items        [2][E*G*slots]
+    DevBuf<int32_t> ro_cnt;                  //             their counters                [split][2][2]
+    int ro_item_grid = 0;                    //             persistent grid of k_observe_items
+    bool ro_prep_stale = true;               // ro_mm / ro_info / items lag the state (per-call calls since)
     DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
     DevBuf<double> ro_mean, ro_stats;
     DevBuf<unsigned long long> ro_steps;
@@ -150,8 +158,61 @@ public:
     DevBuf<RolloutCtx> ro_ctx;               // device copy of {s, ra} read by k_rollout
     RolloutCtx ro_ctx_host{};
     int ro_grid = 0, ro_cap = 0;
+    // large-env path: the envs split into ro_split independent sub-batches, each a pipeline
+    // (k_observe_items -> k_rollout_big) on its own stream, so one sub-batch's latency-bound step
+    // overlaps the other's HBM-bound observation.  Each item launch takes a third of the chip's
+    // k_observe_items slots, leaving room for the other stream's step.  Measured at 256x256 / 4096
+    // agents, 1024 envs (profiles/r01_big_sweeps.txt): 2 streams / 1/3 grid / 64-agent items best.
+    static constexpr int kBigSplit = 2, kItemGridDiv = 3, kItemRows = 64;
+    int ro_split = kBigSplit;
+    hipStream_t ro_str[kMaxSplit] = {};
+    hipEvent_t ro_ev[kMaxSplit + 1] = {};
+    State ro_sub_s[kMaxSplit];
+    RolloutArgs ro_sub_ra[kMaxSplit];
+    DevBuf<RolloutCtx> ro_sub_ctx;
 
-    ~BattleEngine() { release(); if (own_stream && stream) (void)hipStreamDestroy(stream); }
+    ~BattleEngine() {
+        release();
+        for (auto& x : ro_str) if (x) (void)hipStreamDestroy(x);
+        for (auto& x : ro_ev) if (x) (void)hipEventDestroy(x);
+        if (own_stream && stream) (void)hipStreamDestroy(stream);
+    }
+
+    // envs [e0, e0 + n) of s / ra as a batch of their own (every per-env array offset by e0)
+    State sub_state(int e0, int n) const {
+        State q = s;
+        const size_t G = (size_t)n_groups(), c = (size_t)s.cap, a = (size_t)s.acap, cn = (size_t)s.cells_n;
+        q.E = n;
+        q.cells += e0 * cn; q.xy += e0 * c; q.hp += e0 * c; q.next_r += e0 * c; q.last_r += e0 * c;
+        q.last_act += e0 * c; q.op_obj += e0 * c; q.meta += e0 * c; q.grp_ids += e0 * G * c;
+        q.grp_n += e0 * G; q.grp_dead += e0 * G; q.grp_reward += e0 * G; q.id_counter += e0; q.rng += e0;
+        q.atk += e0 * a; q.n_atk += e0; q.mov += e0 * a; q.n_mov += e0; q.done += e0;
+        if (q.food) q.food += e0 * cn;
+        q.idx_mark += e0;
+        return q;
+    }
+    RolloutArgs sub_args(int e0, int k) const {
+        RolloutArgs q = ra;
+        const int G = n_groups();
+        const size_t rc = (size_t)ra.rowcap;
+        int na = 0;
+        for (int g = 0; g < G; g++) {
+            const TypeParams& T = gp.type[g];
+            q.view[g] += e0 * rc * T.view_w * T.view_h * gp.n_ch;
+            q.feat[g] += e0 * rc * gp.feat_size[g];
+            na = std::max(na, T.n_action);
+        }
+        q.actions += e0 * G * rc; q.rewards += e0 * G * rc; q.mean_act += (size_t)e0 * G * na;
+        q.ep_return += (size_t)e0 * G; q.ep_len += e0; q.stats += (size_t)e0 * 4; q.agent_steps += e0;
+        if (q.obs_mm) { q.obs_mm += (size_t)e0 * G * 169; q.obs_info += (size_t)e0 * s.cap; }
+        q.env_base = e0;
+        if (q.big_sort) q.big_sort += (size_t)e0 * s.acap;
+        if (q.obs_items) {
+            q.obs_items += (size_t)e0 * G * ((ra.rowcap + ra.obs_item_rows - 1) / ra.obs_item_rows);
+            q.obs_cnt += 4 * k;
+        }
+        return q;
+    }
 
     void release() {
         for (void* p : {(void*)s.cells, (void*)s.xy, (void*)s.hp, (void*)s.next_r, (void*)s.last_r,
@@ -529,6 +590,7 @@ public:
     }
 
     int reset() {
+        ro_prep_stale = true;
         MFX_CHECK(build_params());
         try {
             const int G = n_groups();
@@ -570,6 +632,7 @@ public:
 
     // same placement for every env (host arrays)
     int add_agents(int group, int n, const char* method, const int* xs, const int* ys, const int* dirs) {
+        ro_prep_stale = true;
         if (!allocated) return fail("add_agents before reset");
         if (group >= n_groups() || group < -1) return fail("invalid group handle in add_agents: %d", group);
         MFX_CHECK(sync_cells());
@@ -668,6 +731,7 @@ public:
         return 0;
     }
     int step(int* d_done) {
+        ro_prep_stale = true;
         if (!allocated) return fail("step before reset");
         MFX_CHECK(sync_cells());
         MFX_HIP(launch_step(gp, d_gp, s, max_ids, d_sort, stream));
@@ -681,6 +745,7 @@ public:
         return 0;
     }
     int clear_dead() {
+        ro_prep_stale = true;
         if (!allocated) return fail("clear_dead before reset");
         MFX_HIP(launch_clear_dead(d_gp, s, stream));
         return 0;
@@ -708,8 +773,10 @@ public:
         try {
             ensure_capacity(total, total);
             const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rowcap);
-            if (smem > 160 * 1024)
-                return fail("rollout: env does not fit in LDS (%zu bytes); use the per-call API", smem);
+            // envs too large for one workgroup's LDS run k_observe + k_rollout_big with the state in HBM
+            ro_big = smem > 160 * 1024;
+            if (ro_big && (!gp.par_step || big_step_smem_bytes(gp, s.cap, s.acap, true) > 160 * 1024))
+                return fail("rollout: env too large for the fused kernels (%zu bytes of LDS); use the per-call API", smem);
             std::vector<int> hx((size_t)G * tcap, 0), hy((size_t)G * tcap, 0);
             for (int g = 0; g < G; g++)
                 for (int i = 0; i < tmpl_n[g]; i++) { hx[(size_t)g * tcap + i] = xs[g][i]; hy[(size_t)g * tcap + i] = ys[g][i]; }
@@ -780,7 +847,39 @@ public:
                 MFX_HIP_THROW(hipMemcpy(ro_walls.p, cells.data(), cells.size() * 2, hipMemcpyHostToDevice));
                 ra.wall_image = ro_walls.p;
             }
-            MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, &ro_grid));
+            if (ro_big) {
+                ro_grid = E;
+                ro_sort.ensure((size_t)E * s.acap);
+                ra.big_sort = ro_sort.p;
+                if (battle_shape(gp)) {
+                    ro_mm.ensure((size_t)E * n_groups() * 169);
+                    ro_info.ensure((size_t)E * s.cap);
+                    ra.obs_mm = ro_mm.p; ra.obs_info = ro_info.p;
+                    const int R = kItemRows;
+                    const size_t slots = (size_t)(ra.rowcap + R - 1) / R;
+                    ro_items.ensure(2 * (size_t)E * n_groups() * slots);
+                    ro_cnt.ensure(4 * kMaxSplit);
+                    ra.obs_items = ro_items.p; ra.obs_cnt = ro_cnt.p;
+                    ra.obs_par_stride = (size_t)E * n_groups() * slots; ra.obs_item_rows = R;
+                    MFX_HIP_THROW(observe_items_grid(gp, R, &ro_item_grid));
+                    ro_item_grid = std::max(1, ro_item_grid / kItemGridDiv);
+                }
+                const int K = std::min(ro_split, E);
+                ro_sub_ctx.ensure(K);
+                std::vector<RolloutCtx> subs(K);
+                for (int k = 0; k < K; k++) {
+                    const int e0 = (int)((long long)E * k / K), e1 = (int)((long long)E * (k + 1) / K);
+                    ro_sub_s[k] = sub_state(e0, e1 - e0);
+                    ro_sub_ra[k] = sub_args(e0, k);
+                    subs[k].s = ro_sub_s[k]; subs[k].ra = ro_sub_ra[k];
+                    if (!ro_str[k]) MFX_HIP_THROW(hipStreamCreateWithFlags(&ro_str[k], hipStreamNonBlocking));
+                }
+                for (auto& x : ro_ev) if (!x) MFX_HIP_THROW(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+                MFX_HIP_THROW(hipMemcpyAsync(ro_sub_ctx.p, subs.data(), sizeof(RolloutCtx) * K, hipMemcpyHostToDevice,
+                                             stream));
+            } else {
+                MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, &ro_grid));
+            }
             ro_cap = s.cap;
             ro_ctx.ensure(1);
             ro_ctx_host.s = s; ro_ctx_host.ra = ra;
@@ -796,6 +895,41 @@ public:
         if (!rollout_ready) return fail("rollout_step before rollout_init");
         if (walls_after_init) return fail("rollout: walls added after rollout_init are not part of the rollout's episodes");
         if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
+        if (ro_big) {
+            MFX_CHECK(sync_cells());
+            const int K = std::min(ro_split, E);
+            if (ra.obs_mm && ro_prep_stale) {
+                if (ra.obs_items) MFX_HIP(hipMemsetAsync(ro_cnt.p, 0, sizeof(int32_t) * 4 * kMaxSplit, stream));
+                for (int k = 0; k < K; k++)
+                    MFX_HIP(launch_obs_prep(d_gp, ro_sub_s[k], ro_sub_ra[k], (int)(ra.step_index & 1), stream));
+            }
+            ro_prep_stale = false;
+            // fork: every sub-batch stream waits for the caller's stream, the caller joins them all
+            MFX_HIP(hipEventRecord(ro_ev[kMaxSplit], stream));
+            for (int k = 0; k < K; k++) MFX_HIP(hipStreamWaitEvent(ro_str[k], ro_ev[kMaxSplit], 0));
+            for (int i = 0; i < n_steps; i++) {
+                for (int k = 0; k < K; k++) {
+                    const State& q = ro_sub_s[k];
+                    const RolloutArgs& qa = ro_sub_ra[k];
+                    if (qa.obs_items) {
+                        MFX_HIP(launch_observe_items(gp, d_gp, q, qa, (int)(ra.step_index & 1), ro_item_grid,
+                                                     ro_str[k]));
+                    } else {                           // generic (non-Battle-shape) observation
+                        for (int g = 0; g < n_groups(); g++)
+                            MFX_HIP(launch_observe(gp, d_gp, q, g, qa.rowcap, qa.view[g], qa.feat[g], qa.rowcap,
+                                                   ro_str[k]));
+                    }
+                    MFX_HIP(launch_rollout_big(gp, d_gp, q, ro_sub_ctx.p + k, ra.step_index, ro_str[k]));
+                }
+                ro_launch++;
+                ra.step_index++;
+            }
+            for (int k = 0; k < K; k++) {
+                MFX_HIP(hipEventRecord(ro_ev[k], ro_str[k]));
+                MFX_HIP(hipStreamWaitEvent(stream, ro_ev[k], 0));
+            }
+            return 0;
+        }
         for (int i = 0; i < n_steps; i++) {
             MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
                                    ro_grid, stream));
@@ -810,7 +944,8 @@ public:
     int rollout_info(int* grid, int* lds_bytes) {
         if (!rollout_ready) return fail("rollout_info before rollout_init");
         *grid = ro_grid;
-        *lds_bytes = (int)rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, ra.rowcap);
+        *lds_bytes = (int)(ro_big ? big_step_smem_bytes(gp, s.cap, s.acap, true)
+                                  : rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, ra.rowcap));
         return 0;
     }
 

@@ -18,6 +18,11 @@ hipError_t launch_set_goal_random(const GameParams* d_gp, const State& s, int g,
 hipError_t launch_rebuild_cells(const GameParams* d_gp, const State& s, const void* walls, hipStream_t st);
 hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
                           float* d_view, float* d_feat, int rowcap, hipStream_t st);
+bool battle_shape(const GameParams& gp);     // the Battle fast-path shape (is_battle_shape)
+hipError_t launch_obs_prep(const GameParams* d_gp, const State& s, const RolloutArgs& ra, int par, hipStream_t st);
+hipError_t launch_observe_items(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
+                                int par, int grid, hipStream_t st);
+hipError_t observe_items_grid(const GameParams& gp, int rows, int* grid);
 hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, const int* d_actions, int rowcap,
                              hipStream_t st);
 hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State& s, int max_ids,
@@ -27,6 +32,9 @@ hipError_t set_stamp_buffer(unsigned long long* d_buf);
 size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap, int rows);
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                           int rows, uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st);
+size_t big_step_smem_bytes(const GameParams& gp, int cap, int acap, bool rollout);
+hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                              uint32_t step_index, hipStream_t st);
 hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int* grid);
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap);
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,

@@ -36,9 +36,15 @@ __device__ unsigned long long* g_stamps;
         psync<kW>();                                                                        \
         if (TID == 0 && g_stamps) g_stamps[stamp_row * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define MFX_BSTAMP(row, i)                                                                  \
+    do {                                                                                    \
+        __syncthreads();                                                                    \
+        if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define MFX_STAMP(i) do {} while (0)
 #define MFX_TSTAMP(kW, i) do {} while (0)
+#define MFX_BSTAMP(row, i) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- utils
@@ -541,6 +547,112 @@ __device__ __forceinline__ void obs_flush(float* __restrict__ dst, const float* 
     }
 }
 
+// Global-cells form of obs_cell, split so that a wave can have kObsPf cell loads in flight: the
+// LDS-side part (record, mask, minimap, address) ...
+struct CellPre {
+    int idx;              // cell index to load (0 when the view cell is masked / off the map)
+    float mo, me;         // minimap channels (own / enemy, +1 at the agent's own bin)
+    bool ok;              // an in-map view cell
+};
+
+__device__ __forceinline__ CellPre obs_cell_pre(const ObsSmem& sm, const float* mm_own, const float* mm_en, int W,
+                                                int H, int gc, int ncell) {
+    constexpr int NV = BattleShape::VW * BattleShape::VH;
+    const bool valid = gc < ncell;
+    const int gs = valid ? gc : 0;
+    const int a = gs / NV, c = gs - a * NV;
+    const int vy = c / BattleShape::VW, vx = c - vy * BattleShape::VW;
+    const uint32_t q = sm.aq[a];
+    const uint32_t mk = (sm.mask[c >> 5] >> (c & 31)) & 1u;
+    const float mo = mm_own[c], me = mm_en[c];
+    const bool self = c == (int)(q >> 24);
+    const int mx = (int)(q & 0xFFFu) - 8 + vx, my = (int)((q >> 12) & 0xFFFu) - 8 + vy;
+    CellPre p;
+    p.ok = valid && mk != 0 && (unsigned)mx < (unsigned)W && (unsigned)my < (unsigned)H;
+    p.idx = p.ok ? my * W + mx : 0;
+    p.mo = valid ? (self ? mo + 1.0f : mo) : 0.0f;
+    p.me = valid ? (self ? me + 1.0f : me) : 0.0f;
+    return p;
+}
+
+// ... and the part after the cell's occupant arrived
+__device__ __forceinline__ CellObs obs_cell_post(const CellPre& p, uint32_t cv, const ObsSmem& sm, int g) {
+    const bool agent = p.ok && cv < kCellFood;
+    const uint32_t inf = sm.info[agent ? cv : 0];
+    CellObs o;
+    o.mo = p.mo;
+    o.me = p.me;
+    o.hn = agent ? __uint_as_float(inf & 0x7FFFFFFFu) : 0.0f;
+    o.kind = (p.ok && cv == kCellWall) ? 1 : (agent ? ((int)(inf >> 31) == g ? 2 : 3) : 0);
+    return o;
+}
+
+typedef __attribute__((address_space(1))) const uint16_t g_u16;
+
+// obs_stream_battle with the cells in HBM (large envs): each wave issues the cell loads of kObsPf
+// 64-cell blocks back to back, then stages and flushes them one by one, so one HBM round trip is
+// paid per kObsPf blocks instead of per block.  The explicit global address space keeps the
+// loads off lgkmcnt (a flat load would be waited for by every LDS sync of the stream).
+constexpr int kObsPf = 4;
+__device__ __forceinline__ void obs_stream_battle_global(const GameParams& gp, const EnvView& v, const ObsSmem& sm,
+                                                         int g, int n, float* __restrict__ out_view,
+                                                         float* __restrict__ out_feat, float* wave_stage) {
+    constexpr int NV = BattleShape::VW * BattleShape::VH, NC = BattleShape::NC, F = BattleShape::F;
+    const int lane = TID & 63, wid = TID >> 6, nw = blockDim.x >> 6;
+    const int W = gp.W, H = gp.H;
+    const TypeParams& T = gp.type[g];
+    const uint16_t* ids = v.grp_ids + g * v.cap;
+    const float* mm_own = sm.mm + g * NV;
+    const float* mm_en = sm.mm + (g ^ 1) * NV;
+    const int ncell = n * NV;
+    g_u16* cells = (g_u16*)v.cells;
+    float* st = wave_stage + wid * kWaveStageFloats;
+    for (int base = wid * kObsPf * kWaveCells; base < ncell; base += nw * kObsPf * kWaveCells) {
+        CellPre p[kObsPf];
+        uint32_t cv[kObsPf];
+#pragma unroll
+        for (int d = 0; d < kObsPf; ++d) p[d] = obs_cell_pre(sm, mm_own, mm_en, W, H, base + d * kWaveCells + lane, ncell);
+#pragma unroll
+        for (int d = 0; d < kObsPf; ++d) cv[d] = cells[p[d].idx];
+#pragma unroll
+        for (int d = 0; d < kObsPf; ++d) {
+            const int b = base + d * kWaveCells;
+            if (b >= ncell) break;
+            obs_stage_cell(st, lane, obs_cell_post(p[d], cv[d], sm, g));
+            wave_sync_lds();
+            obs_flush(out_view + (size_t)b * NC, st, lane, min(kWaveCells, ncell - b));
+            wave_sync_lds();
+        }
+    }
+    // features (GridWorld.cc:411-421): consecutive lanes write consecutive floats
+    const int emb = gp.emb, na = T.n_action;
+    for (int q = TID; q < n * F; q += blockDim.x) {
+        const int a = q / F, f = q - a * F;
+        const int id = ids[a];
+        float val = 0.0f;
+        if (f < emb) val = (float)((id >> f) & 1);
+        if (f == emb + v.last_act[id]) val = 1.0f;
+        if (f == emb + na) val = v.last_r[id];
+        const uint32_t pos = v.xy[id];
+        if (f == emb + na + 1) val = (float)(int)(pos & 0xFFFF) / (float)W;
+        if (f == emb + na + 2) val = (float)(int)(pos >> 16) / (float)H;
+        __builtin_nontemporal_store(val, out_feat + q);
+    }
+}
+
+typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+
+// obs_cell_post with the occupant's info word loaded from HBM too (pipelined like the cells)
+__device__ __forceinline__ CellObs obs_cell_post_g(const CellPre& p, uint32_t cv, uint32_t inf, int g) {
+    const bool agent = p.ok && cv < kCellFood;
+    CellObs o;
+    o.mo = p.mo;
+    o.me = p.me;
+    o.hn = agent ? __uint_as_float(inf & 0x7FFFFFFFu) : 0.0f;
+    o.kind = (p.ok && cv == kCellWall) ? 1 : (agent ? ((int)(inf >> 31) == g ? 2 : 3) : 0);
+    return o;
+}
+
 __device__ __forceinline__ void obs_stream_battle(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int g,
                                                   int n, float* __restrict__ out_view, float* __restrict__ out_feat,
                                                   float* wave_stage) {
@@ -642,6 +754,8 @@ __device__ __forceinline__ void obs_prologue(const GameParams& gp, const ObsSmem
 
 // grid: (chunks, E).  Chunk c covers agents [c*chunk, (c+1)*chunk) of group g.
 // out_view: [E][rowcap][VH][VW][NC], out_feat: [E][rowcap][F]
+// grid: (chunks, E).  Chunk c covers agents [c*chunk, (c+1)*chunk) of group g.
+// out_view: [E][rowcap][VH][VW][NC], out_feat: [E][rowcap][F]
 template <bool kB>
 __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ gpp, State s, int g, int chunk,
                                                  float* __restrict__ out_view, float* __restrict__ out_feat,
@@ -674,9 +788,13 @@ __global__ void __launch_bounds__(256) k_observe(const GameParams* __restrict__ 
     if (kB) {
         EnvView vc = v;                      // rows [a_begin, a_end): shift the group list and outputs
         vc.grp_ids = v.grp_ids + a_begin;
-        obs_agent_records(gp, vc, sm, g, a_end - a_begin);
+        const int na = a_end - a_begin;
+        obs_agent_records(gp, vc, sm, g, na);
         __syncthreads();
-        obs_stream_battle(gp, vc, sm, g, a_end - a_begin, ov + (size_t)a_begin * VF, of + (size_t)a_begin * F, sm.stage);
+        float* ovc = ov + (size_t)a_begin * VF;
+        float* ofc = of + (size_t)a_begin * F;
+        if (cells_in_lds) obs_stream_battle(gp, vc, sm, g, na, ovc, ofc, sm.stage);
+        else obs_stream_battle_global(gp, vc, sm, g, na, ovc, ofc, sm.stage);
     } else {
         for (int a0 = a_begin; a0 < a_end; a0 += kObsK) obs_rows<kB>(gp, v, sm, g, a0, min(kObsK, a_end - a0), ov, of);
     }
@@ -1166,6 +1284,311 @@ __device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView&
 }
 
 // ==================================================================================
+//  parallel step for envs too large for one workgroup's lanes (256x256 / 4096 agents)
+// ==================================================================================
+// Same exact semantics as attack_parallel / move_parallel, with the state in HBM, the whole
+// (1024-lane) workgroup as the team and every per-entry loop strided, so the cost grows
+// O(n log n) instead of O(n^2):
+//  * shuffle: element t sits at jv[t] after Fisher-Yates step t and moves again only at a later
+//    step k with jv[k] == its position.  Buckets L(v) = {k > v : jv[k] == v} (CSR, sorted) give
+//    the first later hit (successor of t in L(jv[t])) and then min L(p) per hop.
+//  * attacks: the hits on every target in shuffle order (CSR by target, <= 8 per target for
+//    1x1 bodies); a sweep re-walks each target's hits under the current death positions.  A
+//    death at position q depends only on deaths at positions < q, so the fixed point is unique
+//    and is the sequential result; a sweep that changes nothing ends the loop.
+//  * moves: ownership rounds as in move_parallel, up to kBigMovPer movers per lane, claims on a
+//    large hashed LDS table.
+constexpr int kBigMovPer = 8;
+constexpr int kBigOwnerSlots = 16384;
+constexpr uint16_t kBigNone = 0xFFFF;       // no death / blank target
+constexpr uint16_t kBigSkip = 0xFFFE;       // attacker already dead at the start of the step
+
+struct BigScratch {
+    uint32_t* ord;     // [A] attack entries in shuffled order
+    uint16_t* jv;      // [A] Fisher-Yates j_k
+    uint32_t* hd;      // [max(A, C) + 1] CSR bucket ends (shuffle buckets, then targets)
+    uint16_t* lst;     // [A] CSR contents
+    uint16_t* att;     // [A] attacker id by position
+    uint16_t* tgt;     // [A] target id at phase start, kBigNone (blank), kBigSkip
+    uint8_t* pg;       // [A] attacker group by position
+    uint16_t* death;   // [C] position of the killing hit, or kBigNone
+    uint32_t* owner;   // [kBigOwnerSlots] move claims (aliases the attack arrays)
+    int* flag;         // [2]
+    int acap;
+    int srow;          // diagnostic stamp row (MFX_STAMPS build), -1 none
+};
+
+__host__ __device__ inline size_t big_scratch_bytes(int acap, int cap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
+    const size_t atk = r16((size_t)acap * 4) + r16((size_t)acap * 2) + r16(m * 4) + 3 * r16((size_t)acap * 2) +
+                       r16((size_t)acap) + r16((size_t)cap * 2);
+    const size_t mov = (size_t)kBigOwnerSlots * 4;
+    return (atk > mov ? atk : mov) + 16;
+}
+
+__device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
+    BigScratch b;
+    size_t o = 0;
+    b.ord = reinterpret_cast<uint32_t*>(base + o);  o += r16((size_t)acap * 4);
+    b.jv = reinterpret_cast<uint16_t*>(base + o);   o += r16((size_t)acap * 2);
+    b.hd = reinterpret_cast<uint32_t*>(base + o);   o += r16(m * 4);
+    b.lst = reinterpret_cast<uint16_t*>(base + o);  o += r16((size_t)acap * 2);
+    b.att = reinterpret_cast<uint16_t*>(base + o);  o += r16((size_t)acap * 2);
+    b.tgt = reinterpret_cast<uint16_t*>(base + o);  o += r16((size_t)acap * 2);
+    b.pg = reinterpret_cast<uint8_t*>(base + o);    o += r16((size_t)acap);
+    b.death = reinterpret_cast<uint16_t*>(base + o); o += r16((size_t)cap * 2);
+    b.owner = reinterpret_cast<uint32_t*>(base);
+    const size_t mov = (size_t)kBigOwnerSlots * 4;
+    b.flag = reinterpret_cast<int*>(base + (o > mov ? o : mov));
+    b.acap = acap;
+    b.srow = -1;
+    return b;
+}
+
+// In-place exclusive scan of a[0..m) over the workgroup (each lane scans a contiguous chunk).
+__device__ __forceinline__ void block_excl_scan(uint32_t* a, int m, int* wave_tot) {
+    const int t = TID, T = blockDim.x, lane = t & 63, wid = t >> 6, nw = T >> 6;
+    const int per = (m + T - 1) / T, b0 = min(m, t * per), b1 = min(m, b0 + per);
+    uint32_t sum = 0;
+    for (int i = b0; i < b1; ++i) sum += a[i];
+    uint32_t inc = sum;                                   // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wave_tot[wid] = (int)inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wid; ++w) off += (uint32_t)wave_tot[w];
+    (void)nw;
+    off += inc - sum;
+    for (int i = b0; i < b1; ++i) { const uint32_t c = a[i]; a[i] = off; off += c; }
+    __syncthreads();
+}
+
+// CSR buckets of keys key(i) in [0, K) for i in [0, n) (key < 0: not bucketed).  Afterwards
+// bucket v is lst[(v ? hd[v-1] : 0) .. hd[v]), ascending in i.
+template <class KeyF>
+__device__ __forceinline__ void big_buckets(const BigScratch& b, int n, int K, KeyF key, int* wave_tot) {
+    const int t = TID, T = blockDim.x;
+    for (int v = t; v <= K; v += T) b.hd[v] = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += T) { const int k = key(i); if (k >= 0) atomicAdd(&b.hd[k], 1u); }
+    __syncthreads();
+    block_excl_scan(b.hd, K, wave_tot);
+    for (int i = t; i < n; i += T) {
+        const int k = key(i);
+        if (k >= 0) b.lst[atomicAdd(&b.hd[k], 1u)] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (int v = t; v < K; v += T) {                      // insertion sort (buckets are short)
+        const int s0 = v ? (int)b.hd[v - 1] : 0, s1 = (int)b.hd[v];
+        for (int i = s0 + 1; i < s1; ++i) {
+            const uint16_t x = b.lst[i];
+            int j = i - 1;
+            while (j >= s0 && b.lst[j] > x) { b.lst[j + 1] = b.lst[j]; --j; }
+            b.lst[j + 1] = x;
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int big_start(const BigScratch& b, int v) { return v ? (int)b.hd[v - 1] : 0; }
+
+// Shuffle + attack resolution for any n (<= acap), whole workgroup.
+__device__ void attack_big(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* atk, int n,
+                           uint32_t& rng, const BigScratch& b, int nid, int* wave_tot) {
+    const int t0 = TID, T = blockDim.x, W = gp.W, H = gp.H;
+    // ---- Fisher-Yates draws (minstd jump-ahead per step)
+    for (int k = t0; k < n; k += T) {
+        const uint32_t x = minstd_jump(rng, (uint32_t)k + 1u);
+        b.jv[k] = (uint16_t)(x % (uint32_t)(k + 1));
+        if (k == n - 1) b.flag[1] = (int)x;
+    }
+    __syncthreads();
+    if (n > 0) rng = (uint32_t)b.flag[1];
+    MFX_BSTAMP(b.srow, 3);
+    big_buckets(b, n, n, [&](int k) { const int j = b.jv[k]; return j < k ? j : -1; }, wave_tot);
+    MFX_BSTAMP(b.srow, 4);
+    for (int t = t0; t < n; t += T) {
+        int p = b.jv[t];
+        bool hop = false;
+        {   // first later swap that hits position p: the successor of t in L(p)
+            const int s1 = (int)b.hd[p];
+            for (int i = big_start(b, p); i < s1; ++i) {
+                const int k = b.lst[i];
+                if (k > t) { p = k; hop = true; break; }
+            }
+        }
+        while (hop) {       // at position p since step p: the next hit is min L(p) (all > p)
+            const int s0 = big_start(b, p);
+            hop = s0 < (int)b.hd[p];
+            if (hop) p = b.lst[s0];
+        }
+        b.ord[p] = atk[t];
+    }
+    __syncthreads();
+    // ---- per position: attacker, group, target at phase start
+    for (int t = t0; t < n; t += T) {
+        const uint32_t e2 = b.ord[t];
+        const int A = (int)(e2 >> 8), ai = (int)(e2 & 0xFF);
+        const uint32_t m = v.meta[A];
+        uint16_t tg = kBigSkip;
+        const int g = meta_group(m);
+        if (!meta_dead(m)) {
+            const SerialType& S = sm.tt[g];
+            const uint32_t pos = v.xy[A];
+            const int ox = (int)(pos & 0xFFFF) + S.att_x_off + S.att_dx[ai];
+            const int oy = (int)(pos >> 16) + S.att_y_off + S.att_dy[ai];
+            uint32_t cv = kCellEmpty;
+            if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
+            tg = kBigNone;
+            if (cv < kCellFood && (S.attack_in_group || (int)meta_group(v.meta[cv]) != g)) tg = (uint16_t)cv;
+        }
+        b.att[t] = (uint16_t)A;
+        b.tgt[t] = tg;
+        b.pg[t] = (uint8_t)g;
+    }
+    for (int id = t0; id < nid; id += T) b.death[id] = kBigNone;
+    __syncthreads();
+    MFX_BSTAMP(b.srow, 5);
+    // ---- hits per target, in shuffle order
+    big_buckets(b, n, nid, [&](int q) { const int x = b.tgt[q]; return x < (int)kBigSkip ? x : -1; }, wave_tot);
+    // ---- fixed point on the death positions (in place; a quiet sweep is the fixed point)
+    for (int it = 0; it <= n + 1; ++it) {
+        if (t0 == 0) b.flag[0] = 0;
+        __syncthreads();
+        for (int X = t0; X < nid; X += T) {
+            const int s0 = big_start(b, X), s1 = (int)b.hd[X];
+            if (s0 == s1) continue;
+            float h = v.hp[X];
+            int d = kBigNone;
+            for (int i = s0; i < s1; ++i) {
+                const int q = b.lst[i];
+                if ((int)b.death[b.att[q]] <= q) continue;        // attacker dead at its turn
+                h = h - sm.tt[b.pg[q]].damage;                    // Agent::be_attack
+                if (h < 0.0f) { d = q; break; }
+            }
+            if (d != (int)b.death[X]) { b.death[X] = (uint16_t)d; b.flag[0] = 1; }
+        }
+        __syncthreads();
+        if (!b.flag[0]) break;
+        __syncthreads();
+    }
+    MFX_BSTAMP(b.srow, 6);
+    // ---- apply: attackers (one attack per agent per step) ...
+    for (int t = t0; t < n; t += T) {
+        const int A = b.att[t], tg = b.tgt[t];
+        if (tg == kBigSkip || (int)b.death[A] <= t) continue;
+        const int g = b.pg[t];
+        const SerialType& S = sm.tt[g];
+        if (tg == kBigNone || (int)b.death[tg] < t) {
+            v.next_r[A] += S.attack_penalty;                      // blank area (or a dead target)
+        } else {
+            const bool kill = (int)b.death[tg] == t;
+            v.meta[A] = (uint8_t)meta_make(0, kill ? kOpKill : kOpAttack, g);
+            v.op_obj[A] = tg;
+            const float reward = kill ? sm.tt[meta_group(v.meta[tg])].kill_reward : 0.0f;
+            v.next_r[A] += reward + S.attack_penalty;
+        }
+    }
+    // ... and every target's hp after its effective hits
+    for (int X = t0; X < nid; X += T) {
+        const int s0 = big_start(b, X), s1 = (int)b.hd[X];
+        if (s0 == s1) continue;
+        float h = v.hp[X];
+        for (int i = s0; i < s1; ++i) {
+            const int q = b.lst[i];
+            if ((int)b.death[b.att[q]] <= q) continue;
+            h = h - sm.tt[b.pg[q]].damage;
+            if (h < 0.0f) break;
+        }
+        v.hp[X] = h;
+    }
+    __syncthreads();
+    // ---- deaths
+    for (int id = t0; id < nid; id += T) {
+        if (b.death[id] == kBigNone) continue;
+        const uint32_t om = v.meta[id];
+        const int og = meta_group(om);
+        v.meta[id] = (uint8_t)meta_make(1, meta_op(om), og);
+        v.next_r[id] = sm.tt[og].dead_penalty;
+        const uint32_t pos = v.xy[id];
+        v.cells[(pos >> 16) * W + (pos & 0xFFFF)] = kCellEmpty;     // remove_agent
+        atomicAdd(&v.grp_dead[og], 1);
+    }
+    __syncthreads();
+}
+
+// Move resolution for n <= kBigMovPer * lanes movers in `order`, whole workgroup.
+__device__ void move_big(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n,
+                         const BigScratch& b) {
+    const int t0 = TID, T = blockDim.x, W = gp.W, H = gp.H;
+    int id[kBigMovPer], src[kBigMovPer], dst[kBigMovPer];
+    uint32_t pend = 0;
+#pragma unroll
+    for (int j = 0; j < kBigMovPer; ++j) {
+        const int i = t0 + j * T;
+        id[j] = -1; src[j] = 0; dst[j] = 0;
+        if (i < n) {
+            const uint32_t ent = order[i];
+            const int a = (int)(ent >> 16), mi = (int)((ent >> 8) & 0xFF);
+            const uint32_t m = v.meta[a];
+            id[j] = a;
+            if (!meta_dead(m)) {
+                const SerialType& S = sm.tt[meta_group(m)];
+                const uint32_t p = v.xy[a];
+                const int x = p & 0xFFFF, y = p >> 16;
+                const int nx = x + S.move_dx[mi], ny = y + S.move_dy[mi];
+                const bool go = !(nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) && !(nx == x && ny == y);
+                src[j] = y * W + x; dst[j] = ny * W + nx;
+                if (go) pend |= 1u << j;
+            }
+        }
+    }
+    for (int round = 0; round <= n; ++round) {
+        for (int k = t0; k < kBigOwnerSlots; k += T) b.owner[k] = 0xFFFFFFFFu;
+        if (t0 == 0) b.flag[0] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kBigMovPer; ++j) {
+            if (!(pend >> j & 1u)) continue;
+            const uint32_t i = (uint32_t)(t0 + j * T);
+            atomicMin(&b.owner[(uint32_t)src[j] % kBigOwnerSlots], i);
+            atomicMin(&b.owner[(uint32_t)dst[j] % kBigOwnerSlots], i);
+        }
+        __syncthreads();
+        bool more = false;
+#pragma unroll
+        for (int j = 0; j < kBigMovPer; ++j) {
+            if (!(pend >> j & 1u)) continue;
+            const uint32_t i = (uint32_t)(t0 + j * T);
+            if (b.owner[(uint32_t)src[j] % kBigOwnerSlots] == i && b.owner[(uint32_t)dst[j] % kBigOwnerSlots] == i) {
+                const uint32_t cv = v.cells[dst[j]];
+                if (cv == kCellEmpty) {
+                    v.cells[src[j]] = kCellEmpty;
+                    v.cells[dst[j]] = (uint16_t)id[j];
+                    v.xy[id[j]] = (uint32_t)(dst[j] % W) | ((uint32_t)(dst[j] / W) << 16);
+                } else if (cv < kCellFood) {
+                    v.meta[id[j]] = (uint8_t)meta_make(0, kOpCollide, meta_group(v.meta[id[j]]));
+                    v.op_obj[id[j]] = (int)cv;
+                }
+                pend &= ~(1u << j);
+            } else {
+                more = true;
+            }
+        }
+        if (more) b.flag[0] = 1;
+        __syncthreads();
+        if (!b.flag[0]) break;
+        __syncthreads();
+    }
+}
+
+// ==================================================================================
 //  reward DSL (GridWorld::calc_reward + calc_rule + calc_event_node, RewardEngine.cc:216-443)
 // ==================================================================================
 // One lane walks the reference's DFS over agent bindings exactly: same level order
@@ -1331,23 +1754,27 @@ __device__ void dsl_rewards(const GameParams& gp, EnvView& v, int mark, int* fla
 // sm.tt must hold the serial type table (load_serial_types + barrier).
 // ps: LDS scratch for the parallel resolution (nullptr: one-lane loops only); nid = id_counter.
 // kDsl: reward rules through the DSL interpreter (gp.dsl), dsl_mark = State::idx_mark of the env.
-template <bool kW, bool kDsl = false>
+template <bool kW, bool kDsl = false, bool kBig = false>
 __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
                               uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
                               int& done_out, const bool have_ps, const ParScratch ps, int nid,
-                              int32_t* ev = nullptr, int dsl_mark = 0) {
+                              int32_t* ev = nullptr, int dsl_mark = 0, const BigScratch* bs = nullptr) {
     const int G = gp.n_groups;
 #ifndef MFX_PAR_MASK
 #define MFX_PAR_MASK 3
 #endif
-    const bool par0 = !ev && have_ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x;
+    const bool par0 = kBig ? (!ev && gp.par_step && n_atk <= bs->acap && n_mov <= kBigMovPer * (int)blockDim.x)
+                           : (!ev && have_ps && gp.par_step && n_atk <= (int)blockDim.x && n_mov <= (int)blockDim.x);
     bool par = par0 && (MFX_PAR_MASK & 1);
     psync<kW>();
     // ---- shuffle + attack (GridWorld.cc:507-558)
 #ifndef MFX_WAVE_STEP_MAX
 #define MFX_WAVE_STEP_MAX 64
 #endif
-    if (kW && par) {
+    if (kBig && par) {
+        attack_big(gp, sm, v, atk, n_atk, rng, *bs, nid, sm.wave_tot);
+        MFX_BSTAMP(bs->srow, 7);
+    } else if (kW && par) {
         attack_parallel<true>(gp, sm, v, atk, n_atk, rng, ps, nid);
     } else if (par && n_atk <= MFX_WAVE_STEP_MAX) {
         if (TID < 64) attack_parallel<true>(gp, sm, v, atk, n_atk, rng, ps, nid);
@@ -1418,7 +1845,11 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         psync<kW>();
     }
     par = par0 && (MFX_PAR_MASK & 2);
-    if (kW && par) {
+    if (kBig && par) {
+        MFX_BSTAMP(bs->srow, 8);
+        move_big(gp, sm, v, order, n_mov, *bs);
+        MFX_BSTAMP(bs->srow, 9);
+    } else if (kW && par) {
         move_parallel<true>(gp, sm, v, order, n_mov, ps);
     } else if (par && n_mov <= MFX_WAVE_STEP_MAX) {
         if (TID < 64) move_parallel<true>(gp, sm, v, order, n_mov, ps);
@@ -1751,15 +2182,17 @@ __device__ __forceinline__ void copy16(void* dst, const void* src, size_t bytes)
 
 // env.reset() + add_agents(custom) of the template (GridWorld.cc:76-124, Map.cc:23-47, 200-247),
 // computed once per rollout_init by one workgroup; k_rollout copies it in at every episode start.
+// in_lds 0: built in place in HBM (images larger than LDS, the k_rollout_big path).
 __global__ void __launch_bounds__(256) k_reset_image(const GameParams* __restrict__ gpp, int cells_n, int cap,
-                                                     RolloutArgs ra, uint4* __restrict__ image) {
+                                                     RolloutArgs ra, uint4* __restrict__ image, int in_lds) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int scal[8];
     const GameParams& gp = *gpp;
     const int G = gp.n_groups, W = gp.W, H = gp.H;
-    EnvView v = carve_env(smem, cells_n, cap, G);
+    char* base = in_lds ? smem : reinterpret_cast<char*>(image);
+    EnvView v = carve_env(base, cells_n, cap, G);
     const size_t bytes = env_image_bytes(cells_n, cap, G);
-    for (size_t i = TID; i < bytes / 4; i += blockDim.x) reinterpret_cast<uint32_t*>(smem)[i] = 0;
+    for (size_t i = TID; i < bytes / 4; i += blockDim.x) reinterpret_cast<uint32_t*>(base)[i] = 0;
     __syncthreads();
     for (int c = TID; c < W * H; c += blockDim.x) {
         const int x = c % W, y = c / W;
@@ -1787,7 +2220,7 @@ __global__ void __launch_bounds__(256) k_reset_image(const GameParams* __restric
         for (int k = 5; k < 8; ++k) scal[k] = 0;
     }
     __syncthreads();
-    copy16(image, smem, bytes);
+    if (in_lds) copy16(image, smem, bytes);
     if (TID < 8) reinterpret_cast<int32_t*>(reinterpret_cast<char*>(image) + bytes)[TID] = scal[TID];
 }
 
@@ -2326,6 +2759,325 @@ hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, 
     return hipGetLastError();
 }
 
+// ==================================================================================
+//  envs too large for one workgroup's LDS (256x256 / 4096 agents): state stays in HBM
+// ==================================================================================
+// One 1024-lane workgroup per env.  LDS holds the step scratch (BigScratch), the move order and,
+// for the rollout, the action buffers; the cells and per-id arrays are read and written in place.
+constexpr int kBigThreads = 1024;
+#ifndef MFX_BIG_ROLLOUT_THREADS
+#define MFX_BIG_ROLLOUT_THREADS 512
+#endif
+// k_rollout_big shares its CUs with the other sub-batch's k_observe: 8 waves of <= 128 VGPRs and
+// ~80 KB of LDS leave room for observation workgroups beside it
+constexpr int kBigRolloutThreads = MFX_BIG_ROLLOUT_THREADS;
+
+struct BigLayout { size_t sm, atk, mov, sorted, ahist, red, big, total; };
+
+__host__ __device__ inline BigLayout big_layout(const GameParams& gp, int cap, int acap, bool rollout) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    BigLayout L;
+    size_t o = 0;
+    L.sm = o;     o += step_sm_bytes(gp.n_groups);
+    L.atk = o;                   // the rollout's attack / move buffers are State::atk / mov (HBM)
+    L.mov = o;
+    L.sorted = o; o += (gp.large_map && !rollout) ? r16((size_t)acap * 4) : 0;   // rollout: RolloutArgs::big_sort
+    L.ahist = o;  o += rollout ? r16((size_t)gp.n_groups * 64 * 4) : 0;
+    L.big = o;    o += r16(big_scratch_bytes(acap, cap));
+    L.red = L.big;                   // block_sum runs after the step: the step scratch is dead
+    L.total = o;
+    return L;
+}
+
+size_t big_step_smem_bytes(const GameParams& gp, int cap, int acap, bool rollout) {
+    return big_layout(gp, cap, acap, rollout).total;
+}
+
+// The inputs every observing chunk of env e shares (Battle shape): the per-group minimap density
+// (obs_minimap) and the packed hp/max | group word of every listed agent, written to HBM once.
+// hist: G * 169 ints of LDS.
+__device__ void obs_prep_env(const GameParams& gp, const EnvView& v, float* __restrict__ mm_out,
+                             uint32_t* __restrict__ info_out, int* hist) {
+    constexpr int VW = BattleShape::VW, VH = BattleShape::VH, NV = VW * VH, G = BattleShape::G;
+    const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
+    for (int i = TID; i < G * NV; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int j = 0; j < G; ++j) {
+        const int n = v.grp_n[j];
+        const float mx = gp.type[j].hp;
+        for (int i = TID; i < n; i += blockDim.x) {
+            const int id = v.grp_ids[j * v.cap + i];
+            const uint32_t p = v.xy[id];
+            atomicAdd(&hist[j * NV + ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw], 1);
+            info_out[id] = __float_as_uint(v.hp[id] / mx) | ((uint32_t)j << 31);
+        }
+    }
+    __syncthreads();
+    for (int i = TID; i < G * NV; i += blockDim.x) {
+        const int n = v.grp_n[i / NV];
+        mm_out[i] = n ? (float)hist[i] / (float)n : __uint_as_float(0xFFC00000u);
+    }
+}
+
+// File env e's observation work items for the step of parity par: one item per obs_item_rows
+// agents of each group (lane 0; one atomic per env).
+__device__ __forceinline__ void obs_file_items(const RolloutArgs& ra, const EnvView& v, int G, int e, int par) {
+    if (TID != 0 || !ra.obs_items) return;
+    const int R = ra.obs_item_rows;
+    int k = 0;
+    for (int g = 0; g < G; ++g) k += (v.grp_n[g] + R - 1) / R;
+    if (!k) return;
+    const int base = atomicAdd(ra.obs_cnt + 2 * par, k);
+    uint32_t* out = ra.obs_items + par * ra.obs_par_stride + base;
+    for (int g = 0, j = 0; g < G; ++g)
+        for (int c = 0; c * R < v.grp_n[g]; ++c) out[j++] = ((uint32_t)e << 12) | ((uint32_t)g << 10) | (uint32_t)c;
+}
+
+__global__ void __launch_bounds__(256) k_obs_prep(const GameParams* __restrict__ gp, State s, RolloutArgs ra, int par) {
+    __shared__ int hist[BattleShape::G * BattleShape::VW * BattleShape::VH];
+    constexpr int NV = BattleShape::VW * BattleShape::VH;
+    const int e = blockIdx.x;
+    const EnvView v = global_view(s, e, gp->n_groups);
+    obs_prep_env(*gp, v, ra.obs_mm + (size_t)e * BattleShape::G * NV, ra.obs_info + (size_t)e * s.cap, hist);
+    obs_file_items(ra, v, gp->n_groups, e, par);
+}
+
+// get_observation of every group of the large envs as a stream of work items (obs_item_rows agents
+// of one group of one env each), taken by persistent workgroups from the list the previous step
+// filed, so the launch stays balanced whatever the spread of group sizes.  The shared inputs
+// (minimap, per-id info) come from obs_prep_env; the cells and the info words are read from HBM
+// kObsPf 64-cell blocks at a time.  Workgroup 0 clears the other parity's counters for the next
+// step's filing (the previous k_rollout_big has finished with them).
+__global__ void __launch_bounds__(256) k_observe_items(const GameParams* __restrict__ gpp, State s, RolloutArgs ra,
+                                                       int par) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int item;
+    constexpr int NV = BattleShape::VW * BattleShape::VH, NC = BattleShape::NC, F = BattleShape::F;
+    const GameParams& gp = *gpp;
+    const int G = BattleShape::G, R = ra.obs_item_rows, W = gp.W, H = gp.H;
+    const int lane = TID & 63, wid = TID >> 6, nw = blockDim.x >> 6;
+    size_t off = 0;
+    ObsSmem sm = carve_obs(smem, gp, 0, 0, R, obs_stage_floats(gp, 0, true, blockDim.x), true, off);
+    obs_prologue(gp, sm, 0);
+    if (blockIdx.x == 0 && TID < 2) ra.obs_cnt[2 * (par ^ 1) + TID] = 0;
+    const int n_items = ra.obs_cnt[2 * par];
+    float* st = sm.stage + wid * kWaveStageFloats;
+    while (true) {
+        if (TID == 0) {
+            const int i = atomicAdd(ra.obs_cnt + 2 * par + 1, 1);
+            item = i < n_items ? (int)ra.obs_items[par * ra.obs_par_stride + i] : -1;
+        }
+        __syncthreads();
+        const int it = item;
+        if (it < 0) break;
+        const int e = it >> 12, g = (it >> 10) & 3, a0 = (it & 1023) * R;
+        const EnvView v = global_view(s, e, G);
+        const int na = min(R, v.grp_n[g] - a0);
+        const float* mmg = ra.obs_mm + (size_t)e * G * NV;
+        for (int i = TID; i < G * NV; i += blockDim.x) sm.mm[i] = mmg[i];
+        EnvView vc = v;
+        vc.grp_ids = v.grp_ids + a0;
+        obs_agent_records(gp, vc, sm, g, na);
+        __syncthreads();
+        const TypeParams& T = gp.type[g];
+        float* ov = ra.view[g] + ((size_t)e * ra.rowcap + a0) * (NV * NC);
+        float* of = ra.feat[g] + ((size_t)e * ra.rowcap + a0) * F;
+        const float* mm_own = sm.mm + g * NV;
+        const float* mm_en = sm.mm + (g ^ 1) * NV;
+        g_u16* cells = (g_u16*)v.cells;
+        g_cu32* info = (g_cu32*)(ra.obs_info + (size_t)e * s.cap);
+        const int ncell = na * NV;
+        for (int base = wid * kObsPf * kWaveCells; base < ncell; base += nw * kObsPf * kWaveCells) {
+            CellPre p[kObsPf];
+            uint32_t cv[kObsPf], inf[kObsPf];
+#pragma unroll
+            for (int d = 0; d < kObsPf; ++d)
+                p[d] = obs_cell_pre(sm, mm_own, mm_en, W, H, base + d * kWaveCells + lane, ncell);
+#pragma unroll
+            for (int d = 0; d < kObsPf; ++d) cv[d] = cells[p[d].idx];
+#pragma unroll
+            for (int d = 0; d < kObsPf; ++d) inf[d] = info[(p[d].ok && cv[d] < kCellFood) ? cv[d] : 0u];
+#pragma unroll
+            for (int d = 0; d < kObsPf; ++d) {
+                const int b = base + d * kWaveCells;
+                if (b >= ncell) break;
+                obs_stage_cell(st, lane, obs_cell_post_g(p[d], cv[d], inf[d], g));
+                wave_sync_lds();
+                obs_flush(ov + (size_t)b * NC, st, lane, min(kWaveCells, ncell - b));
+                wave_sync_lds();
+            }
+        }
+        // features (GridWorld.cc:411-421)
+        const int emb = gp.emb, nact = T.n_action;
+        for (int q = TID; q < na * F; q += blockDim.x) {
+            const int a = q / F, f = q - a * F;
+            const int id = vc.grp_ids[g * v.cap + a];
+            float val = 0.0f;
+            if (f < emb) val = (float)((id >> f) & 1);
+            if (f == emb + v.last_act[id]) val = 1.0f;
+            if (f == emb + nact) val = v.last_r[id];
+            const uint32_t pos = v.xy[id];
+            if (f == emb + nact + 1) val = (float)(int)(pos & 0xFFFF) / (float)W;
+            if (f == emb + nact + 2) val = (float)(int)(pos >> 16) / (float)H;
+            __builtin_nontemporal_store(val, of + q);
+        }
+        __syncthreads();                               // LDS (records, minimap, item) is reused
+    }
+}
+
+// GridWorld::step for one env per workgroup, in place in HBM (the per-call path's large envs).
+__global__ void __launch_bounds__(kBigThreads) k_step_big(const GameParams* __restrict__ gpp, State s) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const GameParams& gp = *gpp;
+    const int e = blockIdx.x;
+    const BigLayout L = big_layout(gp, s.cap, s.acap, false);
+    StepSmem& sm = *reinterpret_cast<StepSmem*>(smem + L.sm);
+    const BigScratch bs = carve_big(smem + L.big, s.acap, s.cap);
+    EnvView v = global_view(s, e, gp.n_groups);
+    uint32_t rng = s.rng[e];
+    int done = 0;
+    load_serial_types(gp, sm);
+    step_env_core<false, false, true>(gp, s, v, s.atk + (size_t)e * s.acap, s.n_atk[e], s.mov + (size_t)e * s.acap,
+                                      s.n_mov[e], reinterpret_cast<uint32_t*>(smem + L.sorted), rng, sm, done, false,
+                                      ParScratch{}, s.id_counter[e], nullptr, 0, &bs);
+    if (TID == 0) {
+        s.rng[e] = rng;
+        s.n_atk[e] = 0;
+        s.n_mov[e] = 0;
+        s.done[e] = done;
+    }
+}
+
+// One training-loop step after get_observation (k_observe, per group) for one env per
+// workgroup: the rush policy + mean action, set_action, step, get_reward, clear_dead, and the
+// episode restart from the reset image -- what agent_phase and the tail of k_rollout do, in HBM.
+__global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GameParams* __restrict__ gpp,
+                                                             const RolloutCtx* __restrict__ ctx, uint32_t step_index) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int misc[4];                       // 0 n_atk, 1 n_mov, 2 episode end
+    const GameParams& gp = *gpp;
+    const State& s = ctx->s;
+    const RolloutArgs& ra = ctx->ra;
+    const int e = blockIdx.x, G = gp.n_groups, cap = s.cap, acap = s.acap;
+    const BigLayout L = big_layout(gp, cap, acap, true);
+    StepSmem& sm = *reinterpret_cast<StepSmem*>(smem + L.sm);
+    uint32_t* atk = s.atk + (size_t)e * acap;
+    uint32_t* mov = s.mov + (size_t)e * acap;
+    uint32_t* sorted = ra.big_sort + (size_t)e * acap;
+    int* ahist = reinterpret_cast<int*>(smem + L.ahist);
+    float* red = reinterpret_cast<float*>(smem + L.red);
+    BigScratch bs = carve_big(smem + L.big, acap, cap);
+#ifdef MFX_STAMPS
+    bs.srow = ra.env_base + e;
+#endif
+    MFX_BSTAMP(bs.srow, 0);
+    EnvView v = global_view(s, e, G);
+    load_serial_types(gp, sm);
+    if (TID == 0) { misc[0] = 0; misc[1] = 0; }
+    int ntot = 0;
+    for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+    // ---------------- policy + mean action (former_act_prob)
+    for (int i = TID; i < G * 64; i += blockDim.x) ahist[i] = 0;
+    __syncthreads();
+    const uint32_t ekey = ra.policy_seed ^ mix32(step_index * 0x9E3779B9u + (uint32_t)(ra.env_base + e) * 0x632BE5ABu);
+    for (int t = TID; t < ntot; t += blockDim.x) {
+        int g = 0, i = t;
+        while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
+        const int id = v.grp_ids[g * cap + i];
+        const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
+        const int a = rush_action(gp, sm.tt[g], v, g, id, key, ra.eps);
+        ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
+        atomicAdd(&ahist[g * 64 + a], 1);
+    }
+    __syncthreads();
+    for (int t = TID; t < G * 64; t += blockDim.x) {
+        const int g = t >> 6, k = t & 63, na = sm.tt[g].n_action, n = v.grp_n[g];
+        if (k < na)   // empty group: np.mean of nothing is NaN
+            ra.mean_act[((size_t)e * G + g) * na + k] =
+                n ? (double)ahist[t] / (double)n : __longlong_as_double(0x7FF8000000000000ll);
+    }
+    MFX_BSTAMP(bs.srow, 1);
+    // ---------------- set_action (group order) and step
+    for (int g = 0; g < G; ++g)
+        set_action_group<false>(gp, s, v, g, ra.actions + ((size_t)e * G + g) * ra.rowcap, atk, misc[0], mov, misc[1],
+                                sm.wave_tot, acap);
+    MFX_BSTAMP(bs.srow, 2);
+    uint32_t rng = s.rng[e];
+    int done = 0;
+    step_env_core<false, false, true>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, false, ParScratch{},
+                                      s.id_counter[e], nullptr, 0, &bs);
+    MFX_BSTAMP(bs.srow, 10);
+    // ---------------- get_reward, episode return, kills
+    float kills = 0.0f, ret[kMaxGroups];
+    for (int g = 0; g < G; ++g) {
+        const int n = v.grp_n[g];
+        float part = 0.0f;
+        for (int i = TID; i < n; i += blockDim.x) {
+            const float r = v.next_r[v.grp_ids[g * cap + i]] + v.grp_reward[g];
+            ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
+            part += r;
+        }
+        ret[g] = block_sum(part, red);
+        kills += (float)v.grp_dead[g];
+    }
+    MFX_BSTAMP(bs.srow, 11);
+    // ---------------- clear_dead
+    clear_dead_env<false>(gp, v, sm.wave_tot);
+    MFX_BSTAMP(bs.srow, 12);
+    // ---------------- episode end -> reset image (env.reset + add_agents of the template)
+    if (TID == 0) {
+        double* st = ra.stats + (size_t)e * 4;
+        st[3] += kills;
+        float* er = ra.ep_return + (size_t)e * G;
+        for (int g = 0; g < G; ++g) er[g] += ret[g];
+        int len = ra.ep_len[e] + 1;
+        misc[2] = 0;
+        if (done || len >= ra.max_steps) {
+            st[0] += 1.0;
+            st[1] += er[0];
+            st[2] += G > 1 ? er[1] : 0.0f;
+            for (int g = 0; g < G; ++g) er[g] = 0.0f;
+            len = 0;
+            misc[2] = 1;
+        }
+        ra.ep_len[e] = len;
+        ra.agent_steps[e] += (unsigned long long)ntot;
+        s.rng[e] = rng;
+        s.n_atk[e] = 0;
+        s.n_mov[e] = 0;
+        s.done[e] = done;
+    }
+    __syncthreads();
+    if (misc[2]) {
+        const EnvView im = carve_env(reinterpret_cast<char*>(const_cast<uint4*>(ra.reset_image)), s.cells_n, cap, G);
+        const int32_t* img_scal = reinterpret_cast<const int32_t*>(
+            reinterpret_cast<const char*>(ra.reset_image) + env_image_bytes(s.cells_n, cap, G));
+        const int idc = img_scal[4];
+        for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = im.cells[i];
+        for (int i = TID; i < idc; i += blockDim.x) {
+            v.xy[i] = im.xy[i]; v.hp[i] = im.hp[i]; v.next_r[i] = im.next_r[i]; v.last_r[i] = im.last_r[i];
+            v.op_obj[i] = im.op_obj[i]; v.last_act[i] = im.last_act[i]; v.meta[i] = im.meta[i];
+        }
+        for (int g = 0; g < G; ++g)
+            for (int i = TID; i < img_scal[g]; i += blockDim.x) v.grp_ids[g * cap + i] = im.grp_ids[g * cap + i];
+        if (TID < G) { v.grp_n[TID] = img_scal[TID]; v.grp_dead[TID] = 0; v.grp_reward[TID] = 0.0f; }
+        if (TID == 0) s.id_counter[e] = idc;
+        __syncthreads();
+    }
+    MFX_BSTAMP(bs.srow, 13);
+    // ---------------- the next observation's shared inputs
+    if (ra.obs_mm) {
+        constexpr int NV = BattleShape::VW * BattleShape::VH;
+        obs_prep_env(gp, v, ra.obs_mm + (size_t)e * G * NV, ra.obs_info + (size_t)e * cap,
+                     reinterpret_cast<int*>(smem + L.big));
+        if (ra.obs_items) {
+            __syncthreads();
+            obs_file_items(ra, v, G, e, (int)((step_index + 1) & 1));
+        }
+    }
+    MFX_BSTAMP(bs.srow, 14);
+}
+
 // State::cells after fused rollout steps: the walls-only image plus every live listed agent.
 __global__ void __launch_bounds__(256) k_rebuild_cells(const GameParams* __restrict__ gp, State s,
                                                        const uint16_t* __restrict__ walls) {
@@ -2362,6 +3114,31 @@ hipError_t launch_set_goal_random(const GameParams* d_gp, const State& s, int g,
     return hipGetLastError();
 }
 
+bool battle_shape(const GameParams& gp) { return is_battle_shape(gp); }
+
+hipError_t launch_obs_prep(const GameParams* d_gp, const State& s, const RolloutArgs& ra, int par, hipStream_t st) {
+    k_obs_prep<<<s.E, 256, 0, st>>>(d_gp, s, ra, par);
+    return hipGetLastError();
+}
+
+hipError_t launch_observe_items(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
+                                int par, int grid, hipStream_t st) {
+    const size_t smem = obs_smem_core(gp, 0, 0, ra.obs_item_rows, obs_stage_floats(gp, 0, true, 256), true);
+    k_observe_items<<<grid, 256, smem, st>>>(d_gp, s, ra, par);
+    return hipGetLastError();
+}
+
+hipError_t observe_items_grid(const GameParams& gp, int rows, int* grid) {
+    const size_t smem = obs_smem_core(gp, 0, 0, rows, obs_stage_floats(gp, 0, true, 256), true);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (err == hipSuccess) err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_observe_items, 256, smem);
+    if (err != hipSuccess) return err;
+    *grid = cus * (per_cu > 0 ? per_cu : 1);
+    return hipSuccess;
+}
+
 hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
                           float* d_view, float* d_feat, int rowcap, hipStream_t st) {
     const int chunk = 64;
@@ -2387,9 +3164,22 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
                        uint32_t* d_sort_scratch, hipStream_t st) {
     const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap) + step_sm_bytes(gp.n_groups);
     const int lds = smem <= 96 * 1024;
+    const size_t big = big_step_smem_bytes(gp, s.cap, s.acap, false);
+    if (!lds && !gp.dsl && gp.par_step && !gp.record_events && big <= 160 * 1024) {
+        k_step_big<<<s.E, kBigThreads, big, st>>>(d_gp, s);      // HBM-resident env, parallel exact step
+        return hipGetLastError();
+    }
     const size_t dyn = lds ? smem : step_sm_bytes(gp.n_groups);
     if (gp.dsl) k_step<true><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
     else k_step<false><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+    return hipGetLastError();
+}
+
+hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                              uint32_t step_index, hipStream_t st) {
+    const size_t smem = big_step_smem_bytes(gp, s.cap, s.acap, true);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    k_rollout_big<<<s.E, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, step_index);
     return hipGetLastError();
 }
 
@@ -2452,8 +3242,8 @@ hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int* gri
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
                               uint4* d_image, hipStream_t st) {
     const size_t smem = env_image_bytes(s.cells_n, s.cap, gp.n_groups);
-    if (smem > 160 * 1024) return hipErrorInvalidValue;
-    k_reset_image<<<1, 256, smem, st>>>(d_gp, s.cells_n, s.cap, ra, d_image);
+    const int in_lds = smem <= 64 * 1024;
+    k_reset_image<<<1, 256, in_lds ? smem : 0, st>>>(d_gp, s.cells_n, s.cap, ra, d_image, in_lds);
     return hipGetLastError();
 }
 

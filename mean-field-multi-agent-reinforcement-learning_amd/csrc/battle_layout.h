@@ -38,6 +38,7 @@ constexpr uint16_t kCellEmpty = 0xFFFF;
 constexpr uint16_t kCellWall = 0xFFFE;
 constexpr uint16_t kCellFood = 0xFFFD;   // food_mode: a food slot (amount in State::food); ids stay below
 constexpr uint32_t kBucketBoundary = 0xFF;
+constexpr int kMaxSplit = 8;              // large-env rollout: most sub-batches (streams)
 
 // last_op encoding in meta bits 1-2
 enum : uint32_t { kOpNull = 0, kOpAttack = 1, kOpKill = 2, kOpCollide = 3 };
@@ -167,6 +168,16 @@ struct RolloutArgs {
     int work_sel;                   //     and zeroes the other one for launch k + 1
     const uint4* reset_image;       // LDS image of the env right after reset + template placement,
                                     // followed by int32 [grp_n[kMaxGroups], id_counter]
+    int env_base;                   // index of env 0 of this (sub-)batch in the whole batch (policy keys)
+    uint32_t* big_sort;             // large envs: [E][acap] band-ordered move buffer of k_rollout_big
+    float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and
+    uint32_t* obs_info;             //   [E][cap] packed hp/max | group << 31 of the NEXT observation,
+                                    //   computed once per env at the end of the step (obs_prep_env)
+    uint32_t* obs_items;            //   [2][E * G * item_slots] observation work items (env << 12 |
+                                    //   group << 10 | chunk) by step parity, filed by obs_file_items
+    int32_t* obs_cnt;               //   [2][2] per parity: items filed, items taken (k_observe_items)
+    size_t obs_par_stride;          //   items per parity region of obs_items
+    int obs_item_rows;              //   agents per item
     const uint4* wall_image;        // [H*W] u16 cells of that image with the agents removed: every
                                     // install rebuilds the cells from it plus the agents' positions, so
                                     // per-env cells are neither read nor written back (State::cells is

@@ -98,3 +98,67 @@ def test_rollout_processes_every_env_once():
     eng.rollout_copy("agent_steps", got)
     eng.sync()
     assert (got == 256 * steps).all(), np.unique(got.numpy())
+
+
+@pytest.mark.parametrize("map_size,n_side,E,T,max_steps", [(256, 2048, 2, 34, 30), (200, 1250, 3, 24, 400)])
+def test_rollout_large_env_matches_oracle(map_size, n_side, E, T, max_steps):
+    """Envs too large for one workgroup's LDS: rollout_step runs k_observe per group and
+    k_rollout_big (state in HBM, 1024-lane parallel exact step).  Checked in lockstep against one
+    oracle env per batch env: views, features, actions' mean, rewards, the episode restart."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    left, right = bd.block_positions(map_size, n_side)
+    eng = BattleBatch(map_size, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=5, stagger=False)
+    grid, lds = eng.rollout_info()
+    assert grid == E and lds > 64 * 1024          # the large-env path was chosen
+    rc = eng.rowcap
+    VF, F = 13 * 13 * 7, 34
+    envs = []
+    for e in range(E):
+        env, h = common.battle_env(common.ORACLE_LIB, map_size)
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        envs.append((env, h))
+    ep_len, kills = [0] * E, 0
+    for t in range(T):
+        eng.rollout_step(1)
+        view = [torch.empty(E * rc * VF, dtype=torch.float32) for _ in range(2)]
+        feat = [torch.empty(E * rc * F, dtype=torch.float32) for _ in range(2)]
+        act = torch.empty(E * 2 * rc, dtype=torch.int32)
+        rew = torch.empty(E * 2 * rc, dtype=torch.float32)
+        mean = torch.empty(E * 2 * 21, dtype=torch.float64)
+        for g in range(2):
+            eng.rollout_copy("view", view[g], group=g)
+            eng.rollout_copy("feature", feat[g], group=g)
+        eng.rollout_copy("actions", act)
+        eng.rollout_copy("rewards", rew)
+        eng.rollout_copy("mean_action", mean)
+        eng.sync()
+        for e, (env, h) in enumerate(envs):
+            acts = []
+            for g in range(2):
+                v, f = env.get_observation(h[g])
+                n = len(v)
+                assert view[g].numpy().reshape(E, rc, VF)[e, :n].tobytes() == v.reshape(n, VF).tobytes(), (e, t, g)
+                assert feat[g].numpy().reshape(E, rc, F)[e, :n].tobytes() == f.tobytes(), (e, t, g)
+                a = act.numpy().reshape(E, 2, rc)[e, g, :n].astype(np.int32)
+                acts.append(a)
+                m = np.bincount(a, minlength=21) / n if n else np.full(21, np.nan)
+                assert np.array_equal(mean.numpy().reshape(E, 2, 21)[e, g], m, equal_nan=True), (e, t, g)
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rw = env.get_reward(h[g])
+                kills += int((~env.get_alive(h[g])).sum())
+                assert rew.numpy().reshape(E, 2, rc)[e, g, :len(rw)].tobytes() == rw.tobytes(), (e, t, g, "reward")
+            env.clear_dead()
+            ep_len[e] += 1
+            if done or ep_len[e] >= max_steps:
+                ep_len[e] = 0
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
+    assert kills > 0                              # the attack fixed point saw real kills
