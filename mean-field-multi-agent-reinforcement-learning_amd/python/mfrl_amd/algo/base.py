@@ -20,6 +20,8 @@ def as_dev(x, dtype=torch.float32):
 
 
 class ValueNet:
+    graph_train = True          # train() replays the minibatch step as a HIP graph (train_batches)
+
     def __init__(self, sess, env, handle, name, update_every=5, use_mf=False, learning_rate=1e-4, tau=0.005,
                  gamma=0.95):
         self.env = env
@@ -40,7 +42,10 @@ class ValueNet:
         self.target_net = copy.deepcopy(self.eval_net)     # TF initialises both; any start works
         for p in self.target_net.parameters():
             p.requires_grad_(False)
-        self.optimizer = torch.optim.Adam(self.eval_net.parameters(), lr=self.lr)
+        # capturable: the step count lives on the device, so train_batches can replay the whole
+        # minibatch update (sample gather, target, loss, backward, Adam, soft update) as a HIP graph
+        self.optimizer = torch.optim.Adam(self.eval_net.parameters(), lr=self.lr, capturable=True)
+        self._graph = None
 
     @property
     def vars(self):
@@ -71,6 +76,81 @@ class ValueNet:
         """Soft update: target = tau * eval + (1 - tau) * target."""
         for t, e in zip(self.target_net.parameters(), self.eval_net.parameters()):
             t.mul_(1.0 - self.tau).add_(self.tau * e)
+
+    # ------------------------------------------------------------------ minibatch loop on device
+    def train_batches(self, buf, batch_num, use_mean):
+        """The reference's train loop (algo/q_learning.py:42-54 DQN, :110-131 MFQ): batch_num times
+        sample -> calc_target_q -> train -> update, printing the loss every 50 minibatches.
+
+        The sample indices are drawn up front with the same np.random.choice calls sample() makes,
+        and the minibatch step is captured once as a HIP graph (static index tensors, the replay
+        rings' fixed storage) and replayed, so a minibatch is one graph launch instead of ~150
+        kernel launches and three host syncs.  The first minibatches run eagerly on a side stream
+        (the warm-up graph capture needs); the losses are read back once at the end."""
+        if batch_num <= 0:
+            return
+        n, B = buf.nb_entries, buf.batch_size
+        idx = np.stack([np.random.choice(n, size=B) for _ in range(batch_num)]).astype(np.int64)
+        nxt = (idx + 1) % n
+        idx_d = torch.as_tensor(idx, device="cuda")
+        nxt_d = torch.as_tensor(nxt, device="cuda")
+        stats = torch.zeros((batch_num, 2), dtype=torch.float32, device="cuda")
+        if self._graph is None:
+            self._s_idx = torch.zeros(B, dtype=torch.int64, device="cuda")
+            self._s_nxt = torch.zeros(B, dtype=torch.int64, device="cuda")
+            self._s_out = torch.zeros(2, dtype=torch.float32, device="cuda")
+        warm = 0 if self._graph is not None else min(3, batch_num)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for i in range(warm):
+                self._s_idx.copy_(idx_d[i])
+                self._s_nxt.copy_(nxt_d[i])
+                self._minibatch(buf, use_mean)
+                stats[i].copy_(self._s_out)
+        torch.cuda.current_stream().wait_stream(side)
+        if warm < batch_num and self._graph is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._minibatch(buf, use_mean)
+            self._graph = g
+        for i in range(warm, batch_num):
+            self._s_idx.copy_(idx_d[i])
+            self._s_nxt.copy_(nxt_d[i])
+            self._graph.replay()
+            stats[i].copy_(self._s_out)
+        st = stats.cpu().numpy()
+        for i in range(0, batch_num, 50):
+            print("[*] LOSS:", float(st[i, 0]), "/ Q:", {"Eval-Q": np.round(float(st[i, 1]), 6)})
+
+    def _minibatch(self, buf, use_mean):
+        """One sample + target + masked-MSE Adam step + soft update on the static index tensors."""
+        i, j = self._s_idx, self._s_nxt
+        obs, feat = buf.obs0.data.index_select(0, i), buf.feat0.data.index_select(0, i)
+        obs_n, feat_n = buf.obs0.data.index_select(0, j), buf.feat0.data.index_select(0, j)
+        acts = buf.actions.data.index_select(0, i).long()
+        rew = buf.rewards.data.index_select(0, i)
+        done = buf.terminals.data.index_select(0, i)
+        mask = buf.masks.data.index_select(0, i).float()
+        prob = buf.prob.data.index_select(0, i) if use_mean else None
+        prob_n = buf.prob.data.index_select(0, j) if use_mean else None
+        with torch.no_grad():
+            t_q = self.target_net(obs_n, feat_n, prob_n)
+            e_qn = self.eval_net(obs_n, feat_n, prob_n)
+            target = mf.mfq_target(e_qn.float().contiguous(), t_q.float().contiguous(), rew, done, self.gamma)
+        e_q = self.eval_net(obs, feat, prob)
+        e_q_max = e_q.gather(1, acts.reshape(-1, 1)).reshape(-1)
+        loss = torch.sum(torch.square(target.float() - e_q_max) * mask) / torch.sum(mask)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        self.optimizer.step()
+        with torch.no_grad():
+            t_p = list(self.target_net.parameters())
+            e_p = list(self.eval_net.parameters())
+            torch._foreach_mul_(t_p, 1.0 - self.tau)
+            torch._foreach_add_(t_p, torch._foreach_mul(e_p, self.tau))
+            self._s_out[0].copy_(loss.detach())
+            self._s_out[1].copy_(e_q_max.detach().mean())
 
     @torch.no_grad()
     def act_dev(self, **kwargs):

@@ -15,6 +15,8 @@ class DQN(base.ValueNet):
     def train(self):
         self.replay_buffer.tight()
         batch_num = self.replay_buffer.get_batch_num()
+        if self.graph_train:
+            return self.train_batches(self.replay_buffer, batch_num, use_mean=False)
         for i in range(batch_num):
             obs, feats, obs_next, feat_next, dones, rewards, actions, masks = self.replay_buffer.sample()
             target_q = self.calc_target_q_dev(obs=obs_next, feature=feat_next, rewards=rewards, dones=dones)
@@ -44,6 +46,8 @@ class MFQ(base.ValueNet):
     def train(self):
         self.replay_buffer.tight()
         batch_num = self.replay_buffer.get_batch_num()
+        if self.graph_train:
+            return self.train_batches(self.replay_buffer, batch_num, use_mean=True)
         for i in range(batch_num):
             obs, feat, acts, act_prob, obs_next, feat_next, act_prob_next, rewards, dones, masks = \
                 self.replay_buffer.sample()

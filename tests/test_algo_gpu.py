@@ -78,3 +78,44 @@ def test_batched_round_in_hbm(algo):
                                                      left_id=0)
     assert max_nums[0] == 6 * 16 and max_nums[1] == 6 * 16       # 0.04 * 24^2 -> 4x4 block per side, 6 envs
     assert all(np.isfinite(mean_r)) and all(np.isfinite(total_r))
+
+
+@pytest.mark.parametrize("algo", ["mfq", "il"])
+def test_graph_train_matches_eager(algo):
+    """train() as one HIP graph per minibatch (ValueNet.train_batches) against the reference-shaped
+    eager loop (sample -> calc_target_q -> train -> update per minibatch): same np.random draws,
+    same parameters afterwards (float tolerance: MIOpen may pick other conv algorithms)."""
+    from mfrl_amd.algo.base import ValueNet as VN
+    np.random.seed(3)
+    torch.manual_seed(3)
+    env, h = _env()
+    m = spawn_ai(algo, None, env, h[0], algo + "-g", 30)
+    opp = spawn_ai(algo, None, env, h[1], algo + "-o", 30)
+    m.train = lambda: None                           # fill the replay only
+    P.play(env, 0, 20, 30, h, [m, opp], print_every=100, eps=0.5, train=True)
+    del m.train
+    buf = m.replay_buffer
+    buf.tight()
+    batch_num = buf.get_batch_num()
+    assert batch_num >= 6
+    twin = spawn_ai(algo, None, env, h[0], algo + "-t", 30)      # same weights, fresh Adam state
+    twin.eval_net.load_state_dict(m.eval_net.state_dict())
+    twin.target_net.load_state_dict(m.target_net.state_dict())
+    state = np.random.get_state()
+    m.train_batches(buf, batch_num, use_mean=(algo == "mfq"))
+    np.random.set_state(state)
+    twin.graph_train = False
+    twin.replay_buffer = buf
+    for i in range(batch_num):                       # the eager loop of q_learning.py, same buffer
+        s = buf.sample()
+        if algo == "mfq":
+            obs, feat, acts, prob, obs_n, feat_n, prob_n, rew, done, mask = s
+            tq = twin.calc_target_q_dev(obs=obs_n, feature=feat_n, rewards=rew, dones=done, prob=prob_n)
+            VN.train(twin, state=[obs, feat], target_q=tq, prob=prob, acts=acts, masks=mask)
+        else:
+            obs, feat, obs_n, feat_n, done, rew, acts, mask = s
+            tq = twin.calc_target_q_dev(obs=obs_n, feature=feat_n, rewards=rew, dones=done)
+            VN.train(twin, state=[obs, feat], target_q=tq, acts=acts, masks=mask)
+        twin.update()
+    for a, b in zip(m.vars, twin.vars):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
