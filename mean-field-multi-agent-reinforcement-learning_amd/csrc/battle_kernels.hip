@@ -36,6 +36,11 @@ __device__ unsigned long long* g_stamps;
         psync<kW>();                                                                        \
         if (TID == 0 && g_stamps) g_stamps[stamp_row * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define MFX_RSTAMP(kW, row, i)                                                              \
+    do {                                                                                    \
+        psync<kW>();                                                                        \
+        if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #define MFX_BSTAMP(row, i)                                                                  \
     do {                                                                                    \
         __syncthreads();                                                                    \
@@ -45,6 +50,7 @@ __device__ unsigned long long* g_stamps;
 #define MFX_STAMP(i) do {} while (0)
 #define MFX_TSTAMP(kW, i) do {} while (0)
 #define MFX_BSTAMP(row, i) do {} while (0)
+#define MFX_RSTAMP(kW, row, i) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- utils
@@ -1323,7 +1329,9 @@ __host__ __device__ inline size_t big_scratch_bytes(int acap, int cap) {
     const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
     const size_t atk = r16((size_t)acap * 4) + r16((size_t)acap * 2) + r16(m * 4) + 3 * r16((size_t)acap * 2) +
                        r16((size_t)acap) + r16((size_t)cap * 2);
-    const size_t mov = (size_t)kBigOwnerSlots * 4;
+    size_t mov = (size_t)kBigOwnerSlots * 4;
+    const size_t bands = (size_t)17 * 1024 * 4;     // band_sort_big counts, up to 16 bands x 1024 lanes
+    if (bands > mov) mov = bands;
     return (atk > mov ? atk : mov) + 16;
 }
 
@@ -1341,7 +1349,8 @@ __device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap) {
     b.pg = reinterpret_cast<uint8_t*>(base + o);    o += r16((size_t)acap);
     b.death = reinterpret_cast<uint16_t*>(base + o); o += r16((size_t)cap * 2);
     b.owner = reinterpret_cast<uint32_t*>(base);
-    const size_t mov = (size_t)kBigOwnerSlots * 4;
+    size_t mov = (size_t)kBigOwnerSlots * 4;
+    if ((size_t)17 * 1024 * 4 > mov) mov = (size_t)17 * 1024 * 4;
     b.flag = reinterpret_cast<int*>(base + (o > mov ? o : mov));
     b.acap = acap;
     b.srow = -1;
@@ -1754,11 +1763,50 @@ __device__ void dsl_rewards(const GameParams& gp, EnvView& v, int mark, int* fla
 // sm.tt must hold the serial type table (load_serial_types + barrier).
 // ps: LDS scratch for the parallel resolution (nullptr: one-lane loops only); nid = id_counter.
 // kDsl: reward rules through the DSL interpreter (gp.dsl), dsl_mark = State::idx_mark of the env.
+// Large-map move order (GridWorld.cc:662-672: band buffers 0..n_sep-1, then the boundary buffer),
+// as ONE stable counting sort over the workgroup: every lane counts the buckets of its contiguous
+// segment of the buffer, one exclusive scan of the bucket-major [bucket][lane] counts gives every
+// (bucket, lane) its output offset, and each lane re-walks its segment.  The counts live in the step
+// scratch (dead between the attacks and the moves).
+constexpr int kMaxBands = 16;
+__device__ __forceinline__ void band_sort_big(const GameParams& gp, const uint32_t* mov, int n, uint32_t* sorted,
+                                              const BigScratch& b, int* wave_tot) {
+    const int T = blockDim.x, t = TID, nb = gp.n_sep + 1;
+    const int per = (n + T - 1) / T, i0 = min(n, t * per), i1 = min(n, i0 + per);
+    uint32_t* cnt = b.ord;                          // [nb][T]
+    int c[kMaxBands + 1];
+#pragma unroll
+    for (int k = 0; k <= kMaxBands; ++k) c[k] = 0;
+    for (int i = i0; i < i1; ++i) {
+        const uint32_t w = mov[i] & 0xFF;
+        const int k = w == kBucketBoundary ? nb - 1 : (int)w;
+#pragma unroll
+        for (int q = 0; q <= kMaxBands; ++q) c[q] += (q == k);
+    }
+#pragma unroll
+    for (int k = 0; k <= kMaxBands; ++k) if (k < nb) cnt[k * T + t] = (uint32_t)c[k];
+    __syncthreads();
+    block_excl_scan(cnt, nb * T, wave_tot);
+#pragma unroll
+    for (int k = 0; k <= kMaxBands; ++k) c[k] = k < nb ? (int)cnt[k * T + t] : 0;
+    for (int i = i0; i < i1; ++i) {
+        const uint32_t ent = mov[i], w = ent & 0xFF;
+        const int k = w == kBucketBoundary ? nb - 1 : (int)w;
+        int o = 0;
+#pragma unroll
+        for (int q = 0; q <= kMaxBands; ++q) if (q == k) o = c[q]++;
+        sorted[o] = ent;
+    }
+    __syncthreads();
+}
+
 template <bool kW, bool kDsl = false, bool kBig = false>
 __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, uint32_t* atk, int n_atk,
                               uint32_t* mov, int n_mov, uint32_t* sorted, uint32_t& rng, StepSmem& sm,
                               int& done_out, const bool have_ps, const ParScratch ps, int nid,
-                              int32_t* ev = nullptr, int dsl_mark = 0, const BigScratch* bs = nullptr) {
+                              int32_t* ev = nullptr, int dsl_mark = 0, const BigScratch* bs = nullptr,
+                              int stamp_row = -1) {
+    (void)stamp_row;
     const int G = gp.n_groups;
 #ifndef MFX_PAR_MASK
 #define MFX_PAR_MASK 3
@@ -1822,7 +1870,10 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
     psync<kW>();
     // ---- move order: large map = band buffers 0..n_sep-1 then boundary (GridWorld.cc:662-672)
     const uint32_t* order = mov;
-    if (gp.large_map) {
+    if (kBig && gp.large_map) {
+        band_sort_big(gp, mov, n_mov, sorted, *bs, sm.wave_tot);
+        order = sorted;
+    } else if (gp.large_map) {
         int base = 0;
         for (int b = 0; b <= gp.n_sep; ++b) {
             const uint32_t want = b < gp.n_sep ? (uint32_t)b : kBucketBoundary;
@@ -1839,6 +1890,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         psync<kW>();
         order = sorted;
     }
+    MFX_RSTAMP(kW, stamp_row, 15);                 // diagnostic: the moves start here
     if (gp.turn_mode) {                            // turns first, same bucket order (GridWorld.cc:597-624)
         if (TID == 0)
             for (int i = 0; i < n_mov; ++i) do_turn_one(gp, sm, v, order[i]);
@@ -2490,7 +2542,8 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
     // ---------------- set_action (group order) and step
     for (int g = 0; g < G; ++g) set_action_group<kW>(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
     MFX_TSTAMP(kW, 5);
-    step_env_core<kW>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, true, ps, sc.id_counter);
+    step_env_core<kW>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, true, ps, sc.id_counter, nullptr,
+                      0, nullptr, stamp_row);
     MFX_TSTAMP(kW, 6);
     // ---------------- get_reward, episode return, kills
     for (int g = 0; g < G; ++g) {
@@ -2948,6 +3001,70 @@ __global__ void __launch_bounds__(kBigThreads) k_step_big(const GameParams* __re
     }
 }
 
+// set_action for every group of env e in group order (GridWorld.cc:430-496) as one pass: each lane
+// classifies a contiguous segment of the concatenated group lists, one exclusive scan over the
+// [moves | attacks][lane] counts places every entry, order kept (the step scratch holds the counts).
+__device__ __forceinline__ void set_action_big(const GameParams& gp, const State& s, EnvView& v, const int32_t* acts,
+                                               int rowcap, uint32_t* atk, uint32_t* mov, int* n_out,
+                                               const BigScratch& b, int* wave_tot) {
+    const int T = blockDim.x, t = TID, G = gp.n_groups, acap = s.acap;
+    int ntot = 0;
+    for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+    const int per = (ntot + T - 1) / T, i0 = min(ntot, t * per), i1 = min(ntot, i0 + per);
+    uint32_t* cnt = b.ord;                              // [2][T]
+    int nm = 0, na = 0;
+    {
+        int g = 0, i = i0;
+        while (g < G && i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
+        for (int k = i0; k < i1; ++k) {
+            while (i >= v.grp_n[g]) { i = 0; ++g; }
+            int a = acts[g * rowcap + i];
+            const TypeParams& TP = gp.type[g];
+            if (a < 0 || a >= TP.n_action) a = TP.turn_base > 6 ? 6 : 0;
+            if (a < TP.attack_base) ++nm; else ++na;
+            ++i;
+        }
+    }
+    cnt[t] = (uint32_t)nm;
+    cnt[T + t] = (uint32_t)na;
+    __syncthreads();
+    block_excl_scan(cnt, 2 * T, wave_tot);
+    const int tot_m = (int)cnt[T];                      // moves before the first attack count
+    int om = (int)cnt[t], oa = (int)cnt[T + t] - tot_m;
+    {
+        int g = 0, i = i0;
+        while (g < G && i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
+        for (int k = i0; k < i1; ++k) {
+            while (i >= v.grp_n[g]) { i = 0; ++g; }
+            const TypeParams& TP = gp.type[g];
+            int a = acts[g * rowcap + i];
+            if (a < 0 || a >= TP.n_action) { set_err(s, 5); a = TP.turn_base > 6 ? 6 : 0; }
+            const int id = v.grp_ids[g * v.cap + i];
+            v.last_act[id] = (uint8_t)a;
+            if (a < TP.attack_base) {                   // moves and turns (same buckets, GridWorld.cc:443-470)
+                uint32_t bucket = kBucketBoundary;
+                if (gp.large_map) {
+                    const int x = v.xy[id] & 0xFFFF, xr = x % gp.band_w;
+                    if (!(xr < 4 || xr > gp.band_w - 4)) bucket = (uint32_t)(x / gp.band_w);
+                }
+                if (om < acap) mov[om] = ((uint32_t)id << 16) | ((uint32_t)a << 8) | bucket;
+                ++om;
+            } else {
+                if (oa < acap) atk[oa] = ((uint32_t)id << 8) | (uint32_t)(a - TP.attack_base);
+                ++oa;
+            }
+            ++i;
+        }
+    }
+    const int tot_a = ntot - tot_m;
+    if (t == 0) {
+        if (tot_m > acap || tot_a > acap) set_err(s, 6);
+        n_out[0] = min(tot_a, acap);
+        n_out[1] = min(tot_m, acap);
+    }
+    __syncthreads();
+}
+
 // One training-loop step after get_observation (k_observe, per group) for one env per
 // workgroup: the rush policy + mean action, set_action, step, get_reward, clear_dead, and the
 // episode restart from the reset image -- what agent_phase and the tail of k_rollout do, in HBM.
@@ -2980,14 +3097,27 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
     for (int i = TID; i < G * 64; i += blockDim.x) ahist[i] = 0;
     __syncthreads();
     const uint32_t ekey = ra.policy_seed ^ mix32(step_index * 0x9E3779B9u + (uint32_t)(ra.env_base + e) * 0x632BE5ABu);
-    for (int t = TID; t < ntot; t += blockDim.x) {
-        int g = 0, i = t;
-        while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
-        const int id = v.grp_ids[g * cap + i];
-        const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
-        const int a = rush_action(gp, sm.tt[g], v, g, id, key, ra.eps);
-        ra.actions[((size_t)e * G + g) * ra.rowcap + i] = a;
-        atomicAdd(&ahist[g * 64 + a], 1);
+    // two agents per lane per pass: both policies' HBM loads (position, 8 attack cells, their
+    // occupants) are in flight together, the stores come after
+    for (int t = TID; t < ntot; t += 2 * blockDim.x) {
+        int a[2], gg[2], ii[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            int g = 0, i = t + j * (int)blockDim.x;
+            a[j] = -1; gg[j] = 0; ii[j] = i;
+            if (i >= ntot) continue;
+            while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
+            const int id = v.grp_ids[g * cap + i];
+            const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
+            a[j] = rush_action(gp, sm.tt[g], v, g, id, key, ra.eps);
+            gg[j] = g; ii[j] = i;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (a[j] < 0) continue;
+            ra.actions[((size_t)e * G + gg[j]) * ra.rowcap + ii[j]] = a[j];
+            atomicAdd(&ahist[gg[j] * 64 + a[j]], 1);
+        }
     }
     __syncthreads();
     for (int t = TID; t < G * 64; t += blockDim.x) {
@@ -2998,9 +3128,7 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
     }
     MFX_BSTAMP(bs.srow, 1);
     // ---------------- set_action (group order) and step
-    for (int g = 0; g < G; ++g)
-        set_action_group<false>(gp, s, v, g, ra.actions + ((size_t)e * G + g) * ra.rowcap, atk, misc[0], mov, misc[1],
-                                sm.wave_tot, acap);
+    set_action_big(gp, s, v, ra.actions + (size_t)e * G * ra.rowcap, ra.rowcap, atk, mov, misc, bs, sm.wave_tot);
     MFX_BSTAMP(bs.srow, 2);
     uint32_t rng = s.rng[e];
     int done = 0;

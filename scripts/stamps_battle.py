@@ -31,6 +31,7 @@ assert eng._dll.mfx_battle_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 
 eng.rollout_step(400)
 torch.cuda.synchronize()
 acc = []
+raw = []
 conc = []
 inst = []
 sub = []
@@ -38,6 +39,7 @@ for t in range(a.steps):
     eng.rollout_step(1)
     torch.cuda.synchronize()
     st = buf.view(a.envs, 16).cpu().numpy().astype(np.int64)
+    raw.append(st)
     acc.append(np.diff(st[:, :11], axis=1))
     sub.append(np.stack([st[:, 13] - st[:, 0], st[:, 1] - st[:, 13], 10 * (st[:, 11] - st[:, 14])], 1))
     rt0, rt1 = st[:, 11], st[:, 12]            # s_memrealtime, 100 MHz
@@ -55,5 +57,8 @@ print("  envs resident at 2/10/30/50/70/90/98%% of the launch:", np.array(inst).
 sb = np.concatenate(sub)
 print("  install split: LDS stores + barrier mean %d, prefetch issue + barrier mean %d; loop top -> stamp 0 "
       "mean %d ns" % tuple(sb.mean(0)))
+mv = np.concatenate([np.stack([st_[:, 15] - st_[:, 5], st_[:, 6] - st_[:, 15]], 1) for st_ in raw])
+ok = (mv > 0).all(1)
+print("step split: shuffle+attack+starve mean %d, moves+rules+done mean %d cycles" % tuple(mv[ok].mean(0)))
 for i, n in enumerate(names[1:]):
     print("%-14s median %8d  mean %8d  share %5.1f%%" % (n, np.median(d[:, i]), d[:, i].mean(), 100 * d[:, i].mean() / tot.mean()))

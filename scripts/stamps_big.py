@@ -21,7 +21,7 @@ ap.add_argument("--map", type=int, default=256)
 ap.add_argument("--agents", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=5)
 a = ap.parse_args()
-names = ["policy+mean", "set_action", "fy draws", "fy buckets", "fy positions", "tgt buckets", "fixed point",
+names = ["policy+mean", "set_action", "fy draws", "fy buckets", "fy positions", "tgt buckets+fixed point",
          "attack apply", "starve+band sort", "moves", "rules+done", "reward", "clear_dead", "restart", "obs prep"]
 eng = BattleBatch(a.map, a.envs, stream=torch.cuda.current_stream())
 left, right = bd.block_positions(a.map, a.agents // 2)
@@ -37,7 +37,7 @@ for t in range(a.steps):
     torch.cuda.synchronize()
     st = buf.view(a.envs, 16).cpu().numpy().astype(np.int64)
     st = st[st[:, 8] > 0]                       # envs whose moves ran in parallel (all stamps present)
-    acc.append(np.diff(st[:, :16], axis=1))
+    acc.append(np.diff(st[:, :15], axis=1))
 d = np.concatenate(acc)
 tot = d.sum(1)
 print("k_rollout_big per env: median %d cycles, mean %d (%d env-steps)" % (np.median(tot), tot.mean(), len(d)))
