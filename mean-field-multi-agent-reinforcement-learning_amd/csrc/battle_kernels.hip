@@ -1322,6 +1322,8 @@ struct BigScratch {
     int* flag;         // [2]
     int acap;
     int srow;          // diagnostic stamp row (MFX_STAMPS build), -1 none
+    char* base;        // the whole scratch region (the moves reuse it), bytes long
+    size_t bytes;
 };
 
 __host__ __device__ inline size_t big_scratch_bytes(int acap, int cap) {
@@ -1354,6 +1356,8 @@ __device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap) {
     b.flag = reinterpret_cast<int*>(base + (o > mov ? o : mov));
     b.acap = acap;
     b.srow = -1;
+    b.base = base;
+    b.bytes = (size_t)(reinterpret_cast<char*>(b.flag) - base);
     return b;
 }
 
@@ -1763,6 +1767,155 @@ __device__ void dsl_rewards(const GameParams& gp, EnvView& v, int mark, int* fla
 // sm.tt must hold the serial type table (load_serial_types + barrier).
 // ps: LDS scratch for the parallel resolution (nullptr: one-lane loops only); nid = id_counter.
 // kDsl: reward rules through the DSL interpreter (gp.dsl), dsl_mark = State::idx_mark of the env.
+// Move resolution without rounds (large envs).  A cell's history in the move phase is short: its
+// occupant at the phase start may leave (at its own move, if that succeeds) and afterwards the FIRST
+// later mover into it takes it for good (nobody moves twice).  So mover m (order index) succeeds iff
+//   * its target was empty at the phase start and no earlier mover targets it, or
+//   * its target's occupant moves at an earlier index m_o, that move succeeds, and no mover between
+//     m_o and m targets the cell;
+// i.e. success(m) = cond(m) AND success(m_o): a forest of AND-chains along "whose cell do I take",
+// evaluated by pointer jumping in O(log chain) rounds instead of one round per link (a 32-column
+// formation advancing into its own rear is a 32-link chain).  Movers are bucketed by target in a
+// hashed LDS list; the latest earlier mover into the same cell (pred) decides cond(m).  A failing
+// mover collides with the cell's occupant at its time: the phase-start occupant, or the first later
+// mover into it (the filler).  Up to 4096 movers (12-bit links).
+constexpr int kJumpSlots = 4096;
+constexpr uint16_t kJumpNone = 0x7FFF;
+__host__ __device__ inline size_t move_jump_bytes(int n, int nid) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    return r16((size_t)kJumpSlots * 4) + r16((size_t)n * 4) + 4 * r16((size_t)n * 2) + r16((size_t)nid * 2);
+}
+
+__device__ __forceinline__ uint32_t jump_hash(uint32_t d) { return (d * 2654435761u) >> 20; }   // 12 bits
+
+__device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n,
+                          const BigScratch& b, int nid) {
+    if (n > 4096 || move_jump_bytes(n, nid) > b.bytes) return false;
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const int T = blockDim.x, t0 = TID, W = gp.W, H = gp.H;
+    char* p = b.base;
+    uint32_t* head = reinterpret_cast<uint32_t*>(p); p += r16((size_t)kJumpSlots * 4);
+    uint32_t* dstv = reinterpret_cast<uint32_t*>(p); p += r16((size_t)n * 4);     // target cell, ~0u if no move
+    uint16_t* nxt = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);      // hashed bucket links
+    uint16_t* st0 = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);      // cond << 15 | link
+    uint16_t* st1 = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);
+    uint16_t* occ = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);      // target's phase-start content
+    uint16_t* mv_of = reinterpret_cast<uint16_t*>(p);                             // [nid] mover index of an id
+    for (int k = t0; k < kJumpSlots; k += T) head[k] = 0xFFFFFFFFu;
+    for (int id = t0; id < nid; id += T) mv_of[id] = kJumpNone;
+    __syncthreads();
+    // ---- movers: target cells, bucket lists, id -> mover
+    for (int m = t0; m < n; m += T) {
+        const uint32_t ent = order[m];
+        const int id = (int)(ent >> 16), mi = (int)((ent >> 8) & 0xFF);
+        const uint32_t meta = v.meta[id];
+        uint32_t d = 0xFFFFFFFFu;
+        if (!meta_dead(meta)) {
+            const SerialType& S = sm.tt[meta_group(meta)];
+            const uint32_t q = v.xy[id];
+            const int x = q & 0xFFFF, y = q >> 16, nx = x + S.move_dx[mi], ny = y + S.move_dy[mi];
+            // out of board: no-op; a move onto itself changes nothing (not a mover here)
+            if (!(nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) && !(nx == x && ny == y)) d = (uint32_t)(ny * W + nx);
+        }
+        dstv[m] = d;
+        if (d != 0xFFFFFFFFu) {
+            mv_of[id] = (uint16_t)m;
+            nxt[m] = (uint16_t)atomicExch(&head[jump_hash(d)], (uint32_t)m);
+        }
+    }
+    __syncthreads();
+    // ---- cond(m) and link m_o from the phase-start cells
+    for (int m = t0; m < n; m += T) {
+        const uint32_t d = dstv[m];
+        uint16_t st = kJumpNone;                           // cond 0, no link: fails
+        uint16_t cv = kCellEmpty;
+        if (d != 0xFFFFFFFFu) {
+            cv = v.cells[d];
+            int pred = -1;                                 // latest earlier mover into d
+            for (uint32_t k = head[jump_hash(d)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
+                if (dstv[k] == d && (int)k < m && (int)k > pred) pred = (int)k;
+            if (cv == kCellEmpty) {
+                st = (uint16_t)((pred < 0 ? 0x8000u : 0u) | kJumpNone);
+            } else if (cv < kCellFood) {
+                const int mo = mv_of[cv];
+                if (mo != kJumpNone && mo < m) st = (uint16_t)((pred < mo ? 0x8000u : 0u) | (uint32_t)mo);
+                else st = kJumpNone;
+            } else {
+                st = kJumpNone;                            // wall
+            }
+        }
+        st0[m] = st;
+        occ[m] = cv;
+    }
+    __syncthreads();
+    // ---- pointer jumping: cond(m) &= cond(link(m)), link(m) = link(link(m))
+    uint16_t* a = st0;
+    uint16_t* c = st1;
+    for (int r = 0; r < 16; ++r) {
+        if (t0 == 0) b.flag[0] = 0;
+        __syncthreads();
+        bool more = false;
+        for (int m = t0; m < n; m += T) {
+            const uint16_t x = a[m];
+            const int l = x & 0x7FFF;
+            uint16_t y = x;
+            if (l != kJumpNone) {
+                const uint16_t z = a[l];
+                y = (uint16_t)((x & z & 0x8000u) | (z & 0x7FFFu));
+                more |= (z & 0x7FFFu) != kJumpNone;
+            }
+            c[m] = y;
+        }
+        if (more) b.flag[0] = 1;
+        __syncthreads();
+        uint16_t* tmp = a; a = c; c = tmp;
+        if (!b.flag[0]) break;
+    }
+    // a[m] >> 15: m succeeds.  ---- collisions (before any cell changes)
+    for (int m = t0; m < n; m += T) {
+        const uint32_t d = dstv[m];
+        if (d == 0xFFFFFFFFu || (a[m] >> 15)) continue;
+        const uint16_t cv = occ[m];
+        int who = -1;                                      // occupant at time m
+        if (cv < kCellFood) {
+            const int mo = mv_of[cv];
+            if (mo == kJumpNone || mo > m || !(a[mo] >> 15)) who = cv;
+            else {
+                int f = 0x7FFFFFFF;                        // the filler: first mover into d after m_o
+                for (uint32_t k = head[jump_hash(d)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
+                    if (dstv[k] == d && (int)k > mo && (int)k < f) f = (int)k;
+                if (f < m) who = (int)(order[f] >> 16);
+            }
+        } else if (cv == kCellEmpty) {
+            int f = 0x7FFFFFFF;                            // the first mover into d took it
+            for (uint32_t k = head[jump_hash(d)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
+                if (dstv[k] == d && (int)k < f) f = (int)k;
+            if (f < m) who = (int)(order[f] >> 16);
+        }
+        if (who >= 0) {
+            const int id = (int)(order[m] >> 16);
+            v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(v.meta[id]));
+            v.op_obj[id] = who;
+        }
+    }
+    // ---- apply: vacate, then fill (a vacated cell may be filled by a later mover)
+    for (int m = t0; m < n; m += T) {
+        if (dstv[m] == 0xFFFFFFFFu || !(a[m] >> 15)) continue;
+        const uint32_t q = v.xy[order[m] >> 16];
+        v.cells[(q >> 16) * W + (q & 0xFFFF)] = kCellEmpty;
+    }
+    __syncthreads();
+    for (int m = t0; m < n; m += T) {
+        const uint32_t d = dstv[m];
+        if (d == 0xFFFFFFFFu || !(a[m] >> 15)) continue;
+        const int id = (int)(order[m] >> 16);
+        v.cells[d] = (uint16_t)id;
+        v.xy[id] = (d % (uint32_t)W) | ((d / (uint32_t)W) << 16);
+    }
+    __syncthreads();
+    return true;
+}
+
 // Large-map move order (GridWorld.cc:662-672: band buffers 0..n_sep-1, then the boundary buffer),
 // as ONE stable counting sort over the workgroup: every lane counts the buckets of its contiguous
 // segment of the buffer, one exclusive scan of the bucket-major [bucket][lane] counts gives every
@@ -1899,7 +2052,10 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
     par = par0 && (MFX_PAR_MASK & 2);
     if (kBig && par) {
         MFX_BSTAMP(bs->srow, 8);
-        move_big(gp, sm, v, order, n_mov, *bs);
+#ifndef MFX_MOVE_JUMP
+#define MFX_MOVE_JUMP 1
+#endif
+        if (!MFX_MOVE_JUMP || !move_jump(gp, sm, v, order, n_mov, *bs, nid)) move_big(gp, sm, v, order, n_mov, *bs);
         MFX_BSTAMP(bs->srow, 9);
     } else if (kW && par) {
         move_parallel<true>(gp, sm, v, order, n_mov, ps);
@@ -3001,70 +3157,6 @@ __global__ void __launch_bounds__(kBigThreads) k_step_big(const GameParams* __re
     }
 }
 
-// set_action for every group of env e in group order (GridWorld.cc:430-496) as one pass: each lane
-// classifies a contiguous segment of the concatenated group lists, one exclusive scan over the
-// [moves | attacks][lane] counts places every entry, order kept (the step scratch holds the counts).
-__device__ __forceinline__ void set_action_big(const GameParams& gp, const State& s, EnvView& v, const int32_t* acts,
-                                               int rowcap, uint32_t* atk, uint32_t* mov, int* n_out,
-                                               const BigScratch& b, int* wave_tot) {
-    const int T = blockDim.x, t = TID, G = gp.n_groups, acap = s.acap;
-    int ntot = 0;
-    for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
-    const int per = (ntot + T - 1) / T, i0 = min(ntot, t * per), i1 = min(ntot, i0 + per);
-    uint32_t* cnt = b.ord;                              // [2][T]
-    int nm = 0, na = 0;
-    {
-        int g = 0, i = i0;
-        while (g < G && i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
-        for (int k = i0; k < i1; ++k) {
-            while (i >= v.grp_n[g]) { i = 0; ++g; }
-            int a = acts[g * rowcap + i];
-            const TypeParams& TP = gp.type[g];
-            if (a < 0 || a >= TP.n_action) a = TP.turn_base > 6 ? 6 : 0;
-            if (a < TP.attack_base) ++nm; else ++na;
-            ++i;
-        }
-    }
-    cnt[t] = (uint32_t)nm;
-    cnt[T + t] = (uint32_t)na;
-    __syncthreads();
-    block_excl_scan(cnt, 2 * T, wave_tot);
-    const int tot_m = (int)cnt[T];                      // moves before the first attack count
-    int om = (int)cnt[t], oa = (int)cnt[T + t] - tot_m;
-    {
-        int g = 0, i = i0;
-        while (g < G && i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
-        for (int k = i0; k < i1; ++k) {
-            while (i >= v.grp_n[g]) { i = 0; ++g; }
-            const TypeParams& TP = gp.type[g];
-            int a = acts[g * rowcap + i];
-            if (a < 0 || a >= TP.n_action) { set_err(s, 5); a = TP.turn_base > 6 ? 6 : 0; }
-            const int id = v.grp_ids[g * v.cap + i];
-            v.last_act[id] = (uint8_t)a;
-            if (a < TP.attack_base) {                   // moves and turns (same buckets, GridWorld.cc:443-470)
-                uint32_t bucket = kBucketBoundary;
-                if (gp.large_map) {
-                    const int x = v.xy[id] & 0xFFFF, xr = x % gp.band_w;
-                    if (!(xr < 4 || xr > gp.band_w - 4)) bucket = (uint32_t)(x / gp.band_w);
-                }
-                if (om < acap) mov[om] = ((uint32_t)id << 16) | ((uint32_t)a << 8) | bucket;
-                ++om;
-            } else {
-                if (oa < acap) atk[oa] = ((uint32_t)id << 8) | (uint32_t)(a - TP.attack_base);
-                ++oa;
-            }
-            ++i;
-        }
-    }
-    const int tot_a = ntot - tot_m;
-    if (t == 0) {
-        if (tot_m > acap || tot_a > acap) set_err(s, 6);
-        n_out[0] = min(tot_a, acap);
-        n_out[1] = min(tot_m, acap);
-    }
-    __syncthreads();
-}
-
 // One training-loop step after get_observation (k_observe, per group) for one env per
 // workgroup: the rush policy + mean action, set_action, step, get_reward, clear_dead, and the
 // episode restart from the reset image -- what agent_phase and the tail of k_rollout do, in HBM.
@@ -3128,7 +3220,9 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
     }
     MFX_BSTAMP(bs.srow, 1);
     // ---------------- set_action (group order) and step
-    set_action_big(gp, s, v, ra.actions + (size_t)e * G * ra.rowcap, ra.rowcap, atk, mov, misc, bs, sm.wave_tot);
+    for (int g = 0; g < G; ++g)
+        set_action_group<false>(gp, s, v, g, ra.actions + ((size_t)e * G + g) * ra.rowcap, atk, misc[0], mov, misc[1],
+                                sm.wave_tot, acap);
     MFX_BSTAMP(bs.srow, 2);
     uint32_t rng = s.rng[e];
     int done = 0;
