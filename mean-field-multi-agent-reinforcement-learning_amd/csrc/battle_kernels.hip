@@ -1326,18 +1326,41 @@ struct BigScratch {
     size_t bytes;
 };
 
-__host__ __device__ inline size_t big_scratch_bytes(int acap, int cap) {
+// Moves by pointer jumping (move_jump) reuse the region: a hashed bucket table of jump_slots(n)
+// heads plus five per-mover arrays and an id -> mover map.
+__host__ __device__ inline int jump_slots(int n) {
+    int s = 64;
+    while (s < 2 * n && s < 4096) s <<= 1;
+    return s;
+}
+__host__ __device__ inline size_t move_jump_bytes(int n, int nid) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
-    const size_t atk = r16((size_t)acap * 4) + r16((size_t)acap * 2) + r16(m * 4) + 3 * r16((size_t)acap * 2) +
-                       r16((size_t)acap) + r16((size_t)cap * 2);
-    size_t mov = (size_t)kBigOwnerSlots * 4;
-    const size_t bands = (size_t)17 * 1024 * 4;     // band_sort_big counts, up to 16 bands x 1024 lanes
-    if (bands > mov) mov = bands;
-    return (atk > mov ? atk : mov) + 16;
+    return r16((size_t)jump_slots(n) * 4) + r16((size_t)n * 4) + 4 * r16((size_t)n * 2) + r16((size_t)nid * 2);
 }
 
-__device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap) {
+// full: the HBM-state path (ownership-round claims and the band sort's counts share the region too);
+// compact: the attack arrays and move_jump only (k_rollout's LDS union).
+__host__ __device__ inline size_t big_attack_bytes(int acap, int cap) {
+    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
+    return r16((size_t)acap * 4) + r16((size_t)acap * 2) + r16(m * 4) + 3 * r16((size_t)acap * 2) +
+           r16((size_t)acap) + r16((size_t)cap * 2);
+}
+__host__ __device__ inline size_t big_region_bytes(int acap, int cap, bool full) {
+    size_t r = big_attack_bytes(acap, cap);
+    const size_t j = move_jump_bytes(acap, cap);
+    if (j > r) r = j;
+    if (full) {
+        if ((size_t)kBigOwnerSlots * 4 > r) r = (size_t)kBigOwnerSlots * 4;
+        if ((size_t)17 * 1024 * 4 > r) r = (size_t)17 * 1024 * 4;     // band_sort_big: 16 bands x 1024 lanes
+    }
+    return (r + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t big_scratch_bytes(int acap, int cap, bool full = true) {
+    return big_region_bytes(acap, cap, full) + 16;
+}
+
+__device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap, bool full = true) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
     BigScratch b;
@@ -1351,13 +1374,11 @@ __device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap) {
     b.pg = reinterpret_cast<uint8_t*>(base + o);    o += r16((size_t)acap);
     b.death = reinterpret_cast<uint16_t*>(base + o); o += r16((size_t)cap * 2);
     b.owner = reinterpret_cast<uint32_t*>(base);
-    size_t mov = (size_t)kBigOwnerSlots * 4;
-    if ((size_t)17 * 1024 * 4 > mov) mov = (size_t)17 * 1024 * 4;
-    b.flag = reinterpret_cast<int*>(base + (o > mov ? o : mov));
+    b.bytes = big_region_bytes(acap, cap, full);
+    b.flag = reinterpret_cast<int*>(base + b.bytes);
     b.acap = acap;
     b.srow = -1;
     b.base = base;
-    b.bytes = (size_t)(reinterpret_cast<char*>(b.flag) - base);
     return b;
 }
 
@@ -1779,29 +1800,24 @@ __device__ void dsl_rewards(const GameParams& gp, EnvView& v, int mark, int* fla
 // hashed LDS list; the latest earlier mover into the same cell (pred) decides cond(m).  A failing
 // mover collides with the cell's occupant at its time: the phase-start occupant, or the first later
 // mover into it (the filler).  Up to 4096 movers (12-bit links).
-constexpr int kJumpSlots = 4096;
 constexpr uint16_t kJumpNone = 0x7FFF;
-__host__ __device__ inline size_t move_jump_bytes(int n, int nid) {
-    auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    return r16((size_t)kJumpSlots * 4) + r16((size_t)n * 4) + 4 * r16((size_t)n * 2) + r16((size_t)nid * 2);
-}
-
-__device__ __forceinline__ uint32_t jump_hash(uint32_t d) { return (d * 2654435761u) >> 20; }   // 12 bits
+__device__ __forceinline__ uint32_t jump_hash(uint32_t d, int bits) { return (d * 2654435761u) >> (32 - bits); }
 
 __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n,
                           const BigScratch& b, int nid) {
     if (n > 4096 || move_jump_bytes(n, nid) > b.bytes) return false;
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const int T = blockDim.x, t0 = TID, W = gp.W, H = gp.H;
+    const int slots = jump_slots(n), hb = __ffs(slots) - 1;
     char* p = b.base;
-    uint32_t* head = reinterpret_cast<uint32_t*>(p); p += r16((size_t)kJumpSlots * 4);
+    uint32_t* head = reinterpret_cast<uint32_t*>(p); p += r16((size_t)slots * 4);
     uint32_t* dstv = reinterpret_cast<uint32_t*>(p); p += r16((size_t)n * 4);     // target cell, ~0u if no move
     uint16_t* nxt = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);      // hashed bucket links
     uint16_t* st0 = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);      // cond << 15 | link
     uint16_t* st1 = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);
     uint16_t* occ = reinterpret_cast<uint16_t*>(p); p += r16((size_t)n * 2);      // target's phase-start content
     uint16_t* mv_of = reinterpret_cast<uint16_t*>(p);                             // [nid] mover index of an id
-    for (int k = t0; k < kJumpSlots; k += T) head[k] = 0xFFFFFFFFu;
+    for (int k = t0; k < slots; k += T) head[k] = 0xFFFFFFFFu;
     for (int id = t0; id < nid; id += T) mv_of[id] = kJumpNone;
     __syncthreads();
     // ---- movers: target cells, bucket lists, id -> mover
@@ -1820,7 +1836,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
         dstv[m] = d;
         if (d != 0xFFFFFFFFu) {
             mv_of[id] = (uint16_t)m;
-            nxt[m] = (uint16_t)atomicExch(&head[jump_hash(d)], (uint32_t)m);
+            nxt[m] = (uint16_t)atomicExch(&head[jump_hash(d, hb)], (uint32_t)m);
         }
     }
     __syncthreads();
@@ -1832,7 +1848,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
         if (d != 0xFFFFFFFFu) {
             cv = v.cells[d];
             int pred = -1;                                 // latest earlier mover into d
-            for (uint32_t k = head[jump_hash(d)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
+            for (uint32_t k = head[jump_hash(d, hb)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
                 if (dstv[k] == d && (int)k < m && (int)k > pred) pred = (int)k;
             if (cv == kCellEmpty) {
                 st = (uint16_t)((pred < 0 ? 0x8000u : 0u) | kJumpNone);
@@ -1870,6 +1886,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
         __syncthreads();
         uint16_t* tmp = a; a = c; c = tmp;
         if (!b.flag[0]) break;
+        __syncthreads();                               // every lane has read the flag before it is reset
     }
     // a[m] >> 15: m succeeds.  ---- collisions (before any cell changes)
     for (int m = t0; m < n; m += T) {
@@ -1882,13 +1899,13 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
             if (mo == kJumpNone || mo > m || !(a[mo] >> 15)) who = cv;
             else {
                 int f = 0x7FFFFFFF;                        // the filler: first mover into d after m_o
-                for (uint32_t k = head[jump_hash(d)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
+                for (uint32_t k = head[jump_hash(d, hb)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
                     if (dstv[k] == d && (int)k > mo && (int)k < f) f = (int)k;
                 if (f < m) who = (int)(order[f] >> 16);
             }
         } else if (cv == kCellEmpty) {
             int f = 0x7FFFFFFF;                            // the first mover into d took it
-            for (uint32_t k = head[jump_hash(d)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
+            for (uint32_t k = head[jump_hash(d, hb)]; k != 0xFFFFFFFFu && k != 0xFFFFu; k = nxt[k])
                 if (dstv[k] == d && (int)k < f) f = (int)k;
             if (f < m) who = (int)(order[f] >> 16);
         }
@@ -1980,6 +1997,8 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
     } else if (par && n_atk <= MFX_WAVE_STEP_MAX) {
         if (TID < 64) attack_parallel<true>(gp, sm, v, atk, n_atk, rng, ps, nid);
         __syncthreads();
+    } else if (par && bs) {                        // whole-workgroup team: O(n log n) form
+        attack_big(gp, sm, v, atk, n_atk, rng, *bs, nid, sm.wave_tot);
     } else if (par) {
         attack_parallel<false>(gp, sm, v, atk, n_atk, rng, ps, nid);
     } else if (TID == 0) {
@@ -2062,6 +2081,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
     } else if (par && n_mov <= MFX_WAVE_STEP_MAX) {
         if (TID < 64) move_parallel<true>(gp, sm, v, order, n_mov, ps);
         __syncthreads();
+    } else if (par && bs && move_jump(gp, sm, v, order, n_mov, *bs, nid)) {
     } else if (par) {
         move_parallel<false>(gp, sm, v, order, n_mov, ps);
     } else {
@@ -2326,7 +2346,10 @@ __host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int 
     u.atk = o;    o += r16((size_t)acap * 4);
     u.mov = o;    o += r16((size_t)acap * 4);
     u.sorted = o; o += gp.large_map ? r16((size_t)acap * 4) : 0;
-    u.par = o;    o += gp.par_step ? r16(par_scratch_bytes(acap, cap)) : 0;
+    // the step scratch: ParScratch (wave-team / small-n forms) or BigScratch in its compact form
+    // (attack_big / move_jump for the whole-workgroup team), never both in one step
+    const size_t pb = par_scratch_bytes(acap, cap), bb = big_scratch_bytes(acap, cap, false);
+    u.par = o;    o += gp.par_step ? r16(pb > bb ? pb : bb) : 0;
     u.total = o;
     return u;
 }
@@ -2666,8 +2689,8 @@ template <bool kB, bool kW>
 __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s, const RolloutArgs& ra, EnvView& v,
                                             EnvScalars& sc, int* misc, StepSmem& sm, int32_t* act, int* ahist,
                                             uint32_t* atk, uint32_t* mov, uint32_t* sorted, float* red,
-                                            const ParScratch ps, int e, uint32_t step_index, int stamp_row,
-                                            uint32_t& rng, int& done, float& kills) {
+                                            const ParScratch ps, const BigScratch* bs, int e, uint32_t step_index,
+                                            int stamp_row, uint32_t& rng, int& done, float& kills) {
     (void)stamp_row;
     const int G = gp.n_groups, cap = s.cap, acap = s.acap;
     // ---------------- policy + mean action (former_act_prob), all groups in one pass
@@ -2699,7 +2722,7 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
     for (int g = 0; g < G; ++g) set_action_group<kW>(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
     MFX_TSTAMP(kW, 5);
     step_env_core<kW>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, true, ps, sc.id_counter, nullptr,
-                      0, nullptr, stamp_row);
+                      0, kW ? nullptr : bs, stamp_row);
     MFX_TSTAMP(kW, 6);
     // ---------------- get_reward, episode return, kills
     for (int g = 0; g < G; ++g) {
@@ -2860,15 +2883,16 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         float kills = 0.0f;
         {
             const ParScratch ps = carve_par(uni + u.par, acap, cap);
+            const BigScratch bs = carve_big(uni + u.par, acap, cap, false);
             int ntot = 0;
             for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
             if (ntot <= 64) {
                 if (TID < 64)
-                    agent_phase<kB, true>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, e,
+                    agent_phase<kB, true>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, &bs, e,
                                           step_index, stamp_row, rng, done, kills);
                 __syncthreads();
             } else {
-                agent_phase<kB, false>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, e,
+                agent_phase<kB, false>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, &bs, e,
                                        step_index, stamp_row, rng, done, kills);
             }
         }
