@@ -2867,7 +2867,9 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
             if (kB) {
                 obs_agent_records(gp, v, osm, g, n);
                 __syncthreads();
+#ifndef MFX_DIAG_NO_OBS                              // diagnostic builds only: everything but the stream
                 obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
+#endif
                 __syncthreads();               // the records are rebuilt for the next group
             } else {
                 obs_prologue(gp, osm, g);
@@ -2886,14 +2888,20 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
             const BigScratch bs = carve_big(uni + u.par, acap, cap, false);
             int ntot = 0;
             for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
+#ifdef MFX_DIAG_OBS_ONLY                             // diagnostic builds only: the observation alone
+            if (false) {
+#else
             if (ntot <= 64) {
+#endif
                 if (TID < 64)
                     agent_phase<kB, true>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, &bs, e,
                                           step_index, stamp_row, rng, done, kills);
                 __syncthreads();
             } else {
+#ifndef MFX_DIAG_OBS_ONLY
                 agent_phase<kB, false>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, &bs, e,
                                        step_index, stamp_row, rng, done, kills);
+#endif
             }
         }
         // ---------------- episode end -> reset + re-place the template (env.reset + add_agents)
@@ -3445,6 +3453,9 @@ hipError_t set_stamp_buffer(unsigned long long* d_buf) {
 
 // The register-prefetch instance needs the env image to fit the prefetch lanes (see EnvPrefetch).
 static bool rollout_prefetch_ok(const GameParams& gp, const State& s) {
+#ifdef MFX_NO_PF
+    return false;                                     // experiments: the synchronous install
+#endif
     const int c4 = s.cap >> 2, nc16 = s.cells_n >> 3;
     return (s.cells_n & 7) == 0 && nc16 + image_small_rows(c4, gp.n_groups) <= kPfRows;
 }
