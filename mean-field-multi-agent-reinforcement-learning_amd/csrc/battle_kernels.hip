@@ -22,29 +22,30 @@ namespace mfx {
 // k_rollout go to a stamp buffer nobody else reads.  The real build compiles these to nothing.
 #ifdef MFX_STAMPS
 __device__ unsigned long long* g_stamps;
+constexpr int kStampW = 32;                  // stamps per env row
 #define MFX_STAMP(i)                                                                        \
     do {                                                                                    \
         __syncthreads();                                                                    \
         if (TID == 0 && g_stamps) {                                                         \
-            g_stamps[stamp_row * 16 + (i)] = __builtin_amdgcn_s_memtime();                  \
-            if ((i) == 0) g_stamps[stamp_row * 16 + 11] = __builtin_amdgcn_s_memrealtime();  \
-            if ((i) == 10) g_stamps[stamp_row * 16 + 12] = __builtin_amdgcn_s_memrealtime(); \
+            g_stamps[stamp_row * kStampW + (i)] = __builtin_amdgcn_s_memtime();                  \
+            if ((i) == 0) g_stamps[stamp_row * kStampW + 11] = __builtin_amdgcn_s_memrealtime();  \
+            if ((i) == 10) g_stamps[stamp_row * kStampW + 12] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                                   \
     } while (0)
 #define MFX_TSTAMP(kW, i)                                                                   \
     do {                                                                                    \
         psync<kW>();                                                                        \
-        if (TID == 0 && g_stamps) g_stamps[stamp_row * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (TID == 0 && g_stamps) g_stamps[stamp_row * kStampW + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #define MFX_RSTAMP(kW, row, i)                                                              \
     do {                                                                                    \
         psync<kW>();                                                                        \
-        if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * kStampW + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #define MFX_BSTAMP(row, i)                                                                  \
     do {                                                                                    \
         __syncthreads();                                                                    \
-        if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * kStampW + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
 #define MFX_STAMP(i) do {} while (0)
@@ -1322,6 +1323,7 @@ struct BigScratch {
     int* flag;         // [2]
     int acap;
     int srow;          // diagnostic stamp row (MFX_STAMPS build), -1 none
+    int sbase;         //   and the first stamp slot of attack_big's internal stamps (minus 3)
     char* base;        // the whole scratch region (the moves reuse it), bytes long
     size_t bytes;
 };
@@ -1378,6 +1380,7 @@ __device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap, b
     b.flag = reinterpret_cast<int*>(base + b.bytes);
     b.acap = acap;
     b.srow = -1;
+    b.sbase = 0;
     b.base = base;
     return b;
 }
@@ -1444,9 +1447,9 @@ __device__ void attack_big(const GameParams& gp, const StepSmem& sm, EnvView& v,
     }
     __syncthreads();
     if (n > 0) rng = (uint32_t)b.flag[1];
-    MFX_BSTAMP(b.srow, 3);
+    MFX_BSTAMP(b.srow, b.sbase + 3);
     big_buckets(b, n, n, [&](int k) { const int j = b.jv[k]; return j < k ? j : -1; }, wave_tot);
-    MFX_BSTAMP(b.srow, 4);
+    MFX_BSTAMP(b.srow, b.sbase + 4);
     for (int t = t0; t < n; t += T) {
         int p = b.jv[t];
         bool hop = false;
@@ -1488,7 +1491,7 @@ __device__ void attack_big(const GameParams& gp, const StepSmem& sm, EnvView& v,
     }
     for (int id = t0; id < nid; id += T) b.death[id] = kBigNone;
     __syncthreads();
-    MFX_BSTAMP(b.srow, 5);
+    MFX_BSTAMP(b.srow, b.sbase + 5);
     // ---- hits per target, in shuffle order
     big_buckets(b, n, nid, [&](int q) { const int x = b.tgt[q]; return x < (int)kBigSkip ? x : -1; }, wave_tot);
     // ---- fixed point on the death positions (in place; a quiet sweep is the fixed point)
@@ -1512,7 +1515,7 @@ __device__ void attack_big(const GameParams& gp, const StepSmem& sm, EnvView& v,
         if (!b.flag[0]) break;
         __syncthreads();
     }
-    MFX_BSTAMP(b.srow, 6);
+    MFX_BSTAMP(b.srow, b.sbase + 6);
     // ---- apply: attackers (one attack per agent per step) ...
     for (int t = t0; t < n; t += T) {
         const int A = b.att[t], tg = b.tgt[t];
@@ -1989,6 +1992,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
 #ifndef MFX_WAVE_STEP_MAX
 #define MFX_WAVE_STEP_MAX 64
 #endif
+    MFX_RSTAMP(kW, stamp_row, 17);                 // diagnostic: the attacks start here
     if (kBig && par) {
         attack_big(gp, sm, v, atk, n_atk, rng, *bs, nid, sm.wave_tot);
         MFX_BSTAMP(bs->srow, 7);
@@ -2013,6 +2017,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
         do_attack_serial(gp, sm, v, atk, n_atk, ev);
     }
     psync<kW>();
+    MFX_RSTAMP(kW, stamp_row, 18);                 // attacks done
     // ---- starve (GridWorld.cc:570-595): independent per agent
     for (int g = 0; g < G; ++g) {
         const TypeParams& T = gp.type[g];
@@ -2089,6 +2094,7 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
             for (int i = 0; i < n_mov; ++i) do_move_one(gp, sm, v, order[i]);
         psync<kW>();
     }
+    MFX_RSTAMP(kW, stamp_row, 19);                 // moves done
     // ---- reward rules (GridWorld::calc_reward, RewardEngine.cc:373-443), rule order
     if (kDsl) {
         if (TID == 0) dsl_rewards(gp, v, dsl_mark, sm.flags);
@@ -2685,6 +2691,9 @@ __device__ __forceinline__ void queue_flush(const RolloutArgs& ra, const int* wg
 
 // Policy, mean action, set_action, step, get_reward and clear_dead of one env, run by a team (see
 // psync): the whole workgroup, or wave 0 alone when the env has at most 64 agents.
+#ifndef MFX_FUSED_BIG
+#define MFX_FUSED_BIG 1            // k_rollout's workgroup teams use attack_big / move_jump
+#endif
 template <bool kB, bool kW>
 __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s, const RolloutArgs& ra, EnvView& v,
                                             EnvScalars& sc, int* misc, StepSmem& sm, int32_t* act, int* ahist,
@@ -2693,6 +2702,9 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
                                             int stamp_row, uint32_t& rng, int& done, float& kills) {
     (void)stamp_row;
     const int G = gp.n_groups, cap = s.cap, acap = s.acap;
+#ifdef MFX_STAMPS
+    if (TID == 0 && g_stamps) g_stamps[stamp_row * kStampW + 16] = (unsigned long long)(v.grp_n[0] + (G > 1 ? v.grp_n[1] : 0));
+#endif
     // ---------------- policy + mean action (former_act_prob), all groups in one pass
     {
         int ntot = 0;
@@ -2722,7 +2734,7 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
     for (int g = 0; g < G; ++g) set_action_group<kW>(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
     MFX_TSTAMP(kW, 5);
     step_env_core<kW>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, true, ps, sc.id_counter, nullptr,
-                      0, kW ? nullptr : bs, stamp_row);
+                      0, (kW || !MFX_FUSED_BIG) ? nullptr : bs, stamp_row);
     MFX_TSTAMP(kW, 6);
     // ---------------- get_reward, episode return, kills
     for (int g = 0; g < G; ++g) {
@@ -2799,7 +2811,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
     }
     while (true) {
 #ifdef MFX_STAMPS
-    if (TID == 0 && g_stamps && e < kconst(ctx).s.E) g_stamps[e * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+    if (TID == 0 && g_stamps && e < kconst(ctx).s.E) g_stamps[e * kStampW + 14] = __builtin_amdgcn_s_memrealtime();
 #endif
     // every iteration re-reads its parameters through scalar loads (see RolloutCtx)
     const GameParams& gp = kconst(gpp);
@@ -2885,7 +2897,10 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         float kills = 0.0f;
         {
             const ParScratch ps = carve_par(uni + u.par, acap, cap);
-            const BigScratch bs = carve_big(uni + u.par, acap, cap, false);
+            BigScratch bs = carve_big(uni + u.par, acap, cap, false);
+#ifdef MFX_STAMPS
+            bs.srow = stamp_row; bs.sbase = 20;        // attack_big's stamps in slots 23-26
+#endif
             int ntot = 0;
             for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
 #ifdef MFX_DIAG_OBS_ONLY                             // diagnostic builds only: the observation alone

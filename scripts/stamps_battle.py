@@ -26,7 +26,7 @@ eng = BattleBatch(64, a.envs, stream=torch.cuda.current_stream())
 left, right = bd.block_positions(64, 128)
 eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1)
 print("rollout grid %d workgroups, %d B dynamic LDS each" % eng.rollout_info())
-buf = torch.zeros(a.envs * 16, dtype=torch.int64, device="cuda")
+buf = torch.zeros(a.envs * 32, dtype=torch.int64, device="cuda")
 assert eng._dll.mfx_battle_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
 eng.rollout_step(400)
 torch.cuda.synchronize()
@@ -36,9 +36,10 @@ conc = []
 inst = []
 sub = []
 for t in range(a.steps):
+    buf.zero_()
     eng.rollout_step(1)
     torch.cuda.synchronize()
-    st = buf.view(a.envs, 16).cpu().numpy().astype(np.int64)
+    st = buf.view(a.envs, 32).cpu().numpy().astype(np.int64)
     raw.append(st)
     acc.append(np.diff(st[:, :11], axis=1))
     sub.append(np.stack([st[:, 13] - st[:, 0], st[:, 1] - st[:, 13], 10 * (st[:, 11] - st[:, 14])], 1))
@@ -57,8 +58,21 @@ print("  envs resident at 2/10/30/50/70/90/98%% of the launch:", np.array(inst).
 sb = np.concatenate(sub)
 print("  install split: LDS stores + barrier mean %d, prefetch issue + barrier mean %d; loop top -> stamp 0 "
       "mean %d ns" % tuple(sb.mean(0)))
-mv = np.concatenate([np.stack([st_[:, 15] - st_[:, 5], st_[:, 6] - st_[:, 15]], 1) for st_ in raw])
-ok = (mv > 0).all(1)
-print("step split: shuffle+attack+starve mean %d, moves+rules+done mean %d cycles" % tuple(mv[ok].mean(0)))
+R = np.concatenate(raw)
+parts = np.stack([R[:, 17] - R[:, 5], R[:, 18] - R[:, 17], R[:, 15] - R[:, 18], R[:, 19] - R[:, 15],
+                  R[:, 6] - R[:, 19]], 1)
+ok = (parts > 0).all(1)
+for lo, hi, tag in ((0, 64, "<= 64 agents (wave team)"), (65, 10 ** 9, "> 64 agents (workgroup team)")):
+    sel = ok & (R[:, 16] >= lo) & (R[:, 16] <= hi)
+    if sel.any():
+        print("step split, %s, %d env-steps: pre %d, attacks %d, starve %d, moves %d, rules+done %d; "
+              "whole env %d" % ((tag, sel.sum()) + tuple(parts[sel].mean(0).astype(int)) +
+                                (int((R[sel, 10] - R[sel, 0]).mean()),)))
+        big = sel & (R[:, 26] > 0)
+        if big.any():               # attack_big internals (workgroup teams): draws, buckets, positions,
+            q = np.stack([R[:, 23] - R[:, 17], R[:, 24] - R[:, 23], R[:, 25] - R[:, 24],   # target buckets +
+                          R[:, 26] - R[:, 25], R[:, 18] - R[:, 26]], 1)[big]               # fixed point, apply
+            print("    attack_big: draws %d, shuffle buckets %d, positions %d, targets+fixed point %d, apply %d"
+                  % tuple(q.mean(0).astype(int)))
 for i, n in enumerate(names[1:]):
     print("%-14s median %8d  mean %8d  share %5.1f%%" % (n, np.median(d[:, i]), d[:, i].mean(), 100 * d[:, i].mean() / tot.mean()))

@@ -26,7 +26,7 @@ names = ["policy+mean", "set_action", "fy draws", "fy buckets", "fy positions", 
 eng = BattleBatch(a.map, a.envs, stream=torch.cuda.current_stream())
 left, right = bd.block_positions(a.map, a.agents // 2)
 eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1)
-buf = torch.zeros(a.envs * 16, dtype=torch.int64, device="cuda")
+buf = torch.zeros(a.envs * 32, dtype=torch.int64, device="cuda")
 assert eng._dll.mfx_battle_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
 eng.rollout_step(400)
 torch.cuda.synchronize()
@@ -35,7 +35,7 @@ for t in range(a.steps):
     buf.zero_()
     eng.rollout_step(1)
     torch.cuda.synchronize()
-    st = buf.view(a.envs, 16).cpu().numpy().astype(np.int64)
+    st = buf.view(a.envs, 32).cpu().numpy().astype(np.int64)
     st = st[st[:, 8] > 0]                       # envs whose moves ran in parallel (all stamps present)
     acc.append(np.diff(st[:, :15], axis=1))
 d = np.concatenate(acc)
