@@ -1806,11 +1806,12 @@ __device__ void dsl_rewards(const GameParams& gp, EnvView& v, int mark, int* fla
 constexpr uint16_t kJumpNone = 0x7FFF;
 __device__ __forceinline__ uint32_t jump_hash(uint32_t d, int bits) { return (d * 2654435761u) >> (32 - bits); }
 
+template <bool kWave>
 __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n,
                           const BigScratch& b, int nid) {
     if (n > 4096 || move_jump_bytes(n, nid) > b.bytes) return false;
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const int T = blockDim.x, t0 = TID, W = gp.W, H = gp.H;
+    const int T = team_lanes<kWave>(), t0 = TID, W = gp.W, H = gp.H;
     const int slots = jump_slots(n), hb = __ffs(slots) - 1;
     char* p = b.base;
     uint32_t* head = reinterpret_cast<uint32_t*>(p); p += r16((size_t)slots * 4);
@@ -1822,7 +1823,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
     uint16_t* mv_of = reinterpret_cast<uint16_t*>(p);                             // [nid] mover index of an id
     for (int k = t0; k < slots; k += T) head[k] = 0xFFFFFFFFu;
     for (int id = t0; id < nid; id += T) mv_of[id] = kJumpNone;
-    __syncthreads();
+    psync<kWave>();
     // ---- movers: target cells, bucket lists, id -> mover
     for (int m = t0; m < n; m += T) {
         const uint32_t ent = order[m];
@@ -1842,7 +1843,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
             nxt[m] = (uint16_t)atomicExch(&head[jump_hash(d, hb)], (uint32_t)m);
         }
     }
-    __syncthreads();
+    psync<kWave>();
     // ---- cond(m) and link m_o from the phase-start cells
     for (int m = t0; m < n; m += T) {
         const uint32_t d = dstv[m];
@@ -1866,13 +1867,13 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
         st0[m] = st;
         occ[m] = cv;
     }
-    __syncthreads();
+    psync<kWave>();
     // ---- pointer jumping: cond(m) &= cond(link(m)), link(m) = link(link(m))
     uint16_t* a = st0;
     uint16_t* c = st1;
     for (int r = 0; r < 16; ++r) {
         if (t0 == 0) b.flag[0] = 0;
-        __syncthreads();
+        psync<kWave>();
         bool more = false;
         for (int m = t0; m < n; m += T) {
             const uint16_t x = a[m];
@@ -1886,10 +1887,10 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
             c[m] = y;
         }
         if (more) b.flag[0] = 1;
-        __syncthreads();
+        psync<kWave>();
         uint16_t* tmp = a; a = c; c = tmp;
         if (!b.flag[0]) break;
-        __syncthreads();                               // every lane has read the flag before it is reset
+        psync<kWave>();                               // every lane has read the flag before it is reset
     }
     // a[m] >> 15: m succeeds.  ---- collisions (before any cell changes)
     for (int m = t0; m < n; m += T) {
@@ -1924,7 +1925,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
         const uint32_t q = v.xy[order[m] >> 16];
         v.cells[(q >> 16) * W + (q & 0xFFFF)] = kCellEmpty;
     }
-    __syncthreads();
+    psync<kWave>();
     for (int m = t0; m < n; m += T) {
         const uint32_t d = dstv[m];
         if (d == 0xFFFFFFFFu || !(a[m] >> 15)) continue;
@@ -1932,7 +1933,7 @@ __device__ bool move_jump(const GameParams& gp, const StepSmem& sm, EnvView& v, 
         v.cells[d] = (uint16_t)id;
         v.xy[id] = (d % (uint32_t)W) | ((d / (uint32_t)W) << 16);
     }
-    __syncthreads();
+    psync<kWave>();
     return true;
 }
 
@@ -2079,14 +2080,14 @@ __device__ void step_env_core(const GameParams& gp, const State& s, EnvView& v, 
 #ifndef MFX_MOVE_JUMP
 #define MFX_MOVE_JUMP 1
 #endif
-        if (!MFX_MOVE_JUMP || !move_jump(gp, sm, v, order, n_mov, *bs, nid)) move_big(gp, sm, v, order, n_mov, *bs);
+        if (!MFX_MOVE_JUMP || !move_jump<false>(gp, sm, v, order, n_mov, *bs, nid)) move_big(gp, sm, v, order, n_mov, *bs);
         MFX_BSTAMP(bs->srow, 9);
-    } else if (kW && par) {
+    } else if (kW && par) {                        // (move_jump<true> measured slower for <= 64 movers)
         move_parallel<true>(gp, sm, v, order, n_mov, ps);
     } else if (par && n_mov <= MFX_WAVE_STEP_MAX) {
         if (TID < 64) move_parallel<true>(gp, sm, v, order, n_mov, ps);
         __syncthreads();
-    } else if (par && bs && move_jump(gp, sm, v, order, n_mov, *bs, nid)) {
+    } else if (par && bs && move_jump<false>(gp, sm, v, order, n_mov, *bs, nid)) {
     } else if (par) {
         move_parallel<false>(gp, sm, v, order, n_mov, ps);
     } else {
@@ -2734,7 +2735,7 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
     for (int g = 0; g < G; ++g) set_action_group<kW>(gp, s, v, g, act + g * cap, atk, misc[0], mov, misc[1], sm.wave_tot, acap);
     MFX_TSTAMP(kW, 5);
     step_env_core<kW>(gp, s, v, atk, misc[0], mov, misc[1], sorted, rng, sm, done, true, ps, sc.id_counter, nullptr,
-                      0, (kW || !MFX_FUSED_BIG) ? nullptr : bs, stamp_row);
+                      0, MFX_FUSED_BIG ? bs : nullptr, stamp_row);
     MFX_TSTAMP(kW, 6);
     // ---------------- get_reward, episode return, kills
     for (int g = 0; g < G; ++g) {
