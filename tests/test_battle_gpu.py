@@ -79,7 +79,9 @@ def _random_scenario(lib_path, map_size, n0, n1, seed, steps, n_walls, episodes=
 
 
 @pytest.mark.parametrize("map_size,n0,n1,seed,walls", [
-    (12, 5, 9, 1, 6), (20, 30, 30, 2, 20), (33, 60, 40, 3, 50), (64, 128, 128, 4, 0), (110, 300, 250, 5, 100)])
+    (12, 5, 9, 1, 6), (20, 30, 30, 2, 20), (33, 60, 40, 3, 50), (64, 128, 128, 4, 0), (110, 300, 250, 5, 100),
+    # envs too large for k_step's LDS copy: k_step_big (attack_big, band sort, move_jump) on random crowds
+    (180, 1500, 1500, 6, 300), (256, 2500, 2000, 7, 600)])
 def test_hip_matches_oracle_random_scenarios(map_size, n0, n1, seed, walls):
     ref = _random_scenario(common.ORACLE_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
     got = _random_scenario(common.HIP_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
