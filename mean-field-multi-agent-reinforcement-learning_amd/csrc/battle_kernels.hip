@@ -1353,6 +1353,7 @@ __host__ __device__ inline size_t big_region_bytes(int acap, int cap, bool full)
     const size_t j = move_jump_bytes(acap, cap);
     if (j > r) r = j;
     if (full) {
+        if ((size_t)cap * 5 > r) r = (size_t)cap * 5;          // k_rollout_big's staged xy + meta
         if ((size_t)kBigOwnerSlots * 4 > r) r = (size_t)kBigOwnerSlots * 4;
         if ((size_t)17 * 1024 * 4 > r) r = (size_t)17 * 1024 * 4;     // band_sort_big: 16 bands x 1024 lanes
     }
@@ -2320,14 +2321,15 @@ __device__ __forceinline__ int rush_action(const GameParams& gp, const SerialTyp
     return a;
 }
 
-__device__ __forceinline__ float block_sum(float x, float* red) {     // fixed-order reduction
-    red[TID] = x;
+// Fixed-order workgroup sum in two barriers: butterfly within each wave, then the wave partials in
+// wave order (red: one float per wave).
+__device__ __forceinline__ float block_sum_waves(float x, float* red) {
+    const int nw = blockDim.x >> 6;
+    x = wave_sum(x);
+    if ((TID & 63) == 0) red[TID >> 6] = x;
     __syncthreads();
-    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
-        if ((int)TID < w) red[TID] += red[TID + w];
-        __syncthreads();
-    }
-    const float r = red[0];
+    float r = 0.0f;
+    for (int w = 0; w < nw; ++w) r += red[w];
     __syncthreads();
     return r;
 }
@@ -2746,7 +2748,7 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
             if (i < ra.rowcap) ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
             part += r;
         }
-        const float tot = kW ? wave_sum(part) : block_sum(part, red);
+        const float tot = kW ? wave_sum(part) : block_sum_waves(part, red);
         if (TID == 0) { sc.ep_return[g] += tot; kills += (float)v.grp_dead[g]; }
     }
     MFX_TSTAMP(kW, 7);
@@ -3234,6 +3236,16 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
     int ntot = 0;
     for (int g = 0; g < G; ++g) ntot += v.grp_n[g];
     // ---------------- policy + mean action (former_act_prob)
+    // meta and positions of every id staged in LDS (the step scratch is free until the attacks): the
+    // policy's and set_action's dependent lookups become LDS reads; the cells stay in HBM
+    EnvView vp = v;                        // (big_region_bytes holds cap * 5 bytes)
+    {
+        const int idc = s.id_counter[e];
+        uint32_t* xy_l = reinterpret_cast<uint32_t*>(bs.base);
+        uint8_t* meta_l = reinterpret_cast<uint8_t*>(bs.base + (size_t)cap * 4);
+        for (int i = TID; i < idc; i += blockDim.x) { xy_l[i] = v.xy[i]; meta_l[i] = v.meta[i]; }
+        vp.xy = xy_l; vp.meta = meta_l;
+    }
     for (int i = TID; i < G * 64; i += blockDim.x) ahist[i] = 0;
     __syncthreads();
     const uint32_t ekey = ra.policy_seed ^ mix32(step_index * 0x9E3779B9u + (uint32_t)(ra.env_base + e) * 0x632BE5ABu);
@@ -3249,7 +3261,7 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
             while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
             const int id = v.grp_ids[g * cap + i];
             const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
-            a[j] = rush_action(gp, sm.tt[g], v, g, id, key, ra.eps);
+            a[j] = rush_action(gp, sm.tt[g], vp, g, id, key, ra.eps);
             gg[j] = g; ii[j] = i;
         }
 #pragma unroll
@@ -3268,8 +3280,8 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
     }
     MFX_BSTAMP(bs.srow, 1);
     // ---------------- set_action (group order) and step
-    for (int g = 0; g < G; ++g)
-        set_action_group<false>(gp, s, v, g, ra.actions + ((size_t)e * G + g) * ra.rowcap, atk, misc[0], mov, misc[1],
+    for (int g = 0; g < G; ++g)            // vp: positions from LDS, last_act written to HBM
+        set_action_group<false>(gp, s, vp, g, ra.actions + ((size_t)e * G + g) * ra.rowcap, atk, misc[0], mov, misc[1],
                                 sm.wave_tot, acap);
     MFX_BSTAMP(bs.srow, 2);
     uint32_t rng = s.rng[e];
@@ -3287,7 +3299,7 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
             ra.rewards[((size_t)e * G + g) * ra.rowcap + i] = r;
             part += r;
         }
-        ret[g] = block_sum(part, red);
+        ret[g] = block_sum_waves(part, red);
         kills += (float)v.grp_dead[g];
     }
     MFX_BSTAMP(bs.srow, 11);
