@@ -131,6 +131,20 @@ public:
     int pending_ub = 0;                              // upper bound of queued actions
     // drop-in staging (env 0, host buffers)
     DevBuf<float> st_view, st_feat, st_f32;
+    // Drop-in host cache (env 0).  The reference call sequence asks the same state many times per step
+    // (get_num before every getter, both groups' observations, ids / rewards / alive of both groups);
+    // every state change bumps `epoch`, and a getter fetches everything it may be asked next for the
+    // current epoch in ONE device-to-host transfer into pinned memory with ONE stream sync: two syncs
+    // per training-loop step (observations + ids before the actions, done + rewards / alive / positions
+    // after the step) instead of one or two per call.
+    uint64_t epoch = 1, n_ep = 0, obs_ep = 0, info_ep = 0;
+    int hn[kMaxGroups] = {};                 // group sizes of env 0 (valid when n_ep == epoch)
+    size_t obs_rows = 0, info_rows = 0;      // rows per group of the staging layouts below
+    DevBuf<uint8_t> st_info;                 // env 0's record (k_get_env0): header, then per group
+                                             //   ids i32 | reward f32 | pos 2 x i32 | alive u8, x rows
+    PinBuf<uint8_t> pin_obs, pin_info;       // host copies: views + features, info, in the same layouts
+    PinBuf<int32_t> pin_act;                 // [G][rows] actions on their way to the device
+    hipEvent_t act_ev[kMaxGroups] = {};      // that copy of group g has left pin_act
     DevBuf<int> st_i32, st_xs, st_ys, st_dirs;
     DevBuf<uint8_t> st_u8;
     // fused rollout (bench / throughput path)
@@ -172,6 +186,7 @@ public:
     DevBuf<RolloutCtx> ro_sub_ctx;
 
     ~BattleEngine() {
+        for (auto& x : act_ev) if (x) (void)hipEventDestroy(x);
         release();
         for (auto& x : ro_str) if (x) (void)hipStreamDestroy(x);
         for (auto& x : ro_ev) if (x) (void)hipEventDestroy(x);
@@ -236,6 +251,7 @@ public:
 
     // ------------------------------------------------------------------ config
     int set_config(const char* key, void* p) {
+        touch();
         if (!strcmp(key, "map_width")) W = *(int*)p;
         else if (!strcmp(key, "map_height")) H = *(int*)p;
         else if (!strcmp(key, "food_mode")) food = *(bool*)p;
@@ -258,6 +274,7 @@ public:
     }
 
     int register_type(const char* name, int n, const char** keys, const float* values) {
+        touch();
         if (types.count(name)) return fail("duplicated name of agent type: %s", name);
         AgentTypeSpec t;
         t.name = name;
@@ -306,6 +323,7 @@ public:
     }
 
     int new_group(const char* type_name, int* group) {
+        touch();
         if (!types.count(type_name)) return fail("invalid name of agent type in new_group: %s", type_name);
         if (n_groups() >= kMaxGroups) return fail("at most %d groups", kMaxGroups);
         if (allocated) return fail("new_group after the first reset is not supported");
@@ -590,6 +608,7 @@ public:
     }
 
     int reset() {
+        touch();
         ro_prep_stale = true;
         MFX_CHECK(build_params());
         try {
@@ -632,6 +651,7 @@ public:
 
     // same placement for every env (host arrays)
     int add_agents(int group, int n, const char* method, const int* xs, const int* ys, const int* dirs) {
+        touch();
         ro_prep_stale = true;
         if (!allocated) return fail("add_agents before reset");
         if (group >= n_groups() || group < -1) return fail("invalid group handle in add_agents: %d", group);
@@ -679,6 +699,7 @@ public:
 
     // GridWorld::set_goal (GridWorld.cc:729-740): "random" only, goals never read back.
     int set_goal(int group, const char* method) {
+        touch();
         if (strcmp(method, "random")) return fail("invalid goal type in GridWorld::set_goal");
         if (!allocated || group < 0 || group >= n_groups()) return fail("set_goal: bad state or group");
         MFX_HIP(launch_set_goal_random(d_gp, s, group, stream));
@@ -700,11 +721,116 @@ public:
         return 0;
     }
 
-    int num_env0(int g) {
-        int32_t n = 0;
-        MFX_HIP(hipMemcpyAsync(&n, s.grp_n + g, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    void touch() { ++epoch; }                // any state change of env 0 (drop-in host cache)
+
+    int report_err(int32_t h) {
+        if (!h) return 0;
+        MFX_HIP(hipMemsetAsync(d_err, 0, sizeof(int32_t), stream));
+        static const char* msg[] = {"", "", "agent capacity exceeded", "no blank position for random placement",
+                                    "output row capacity smaller than the group", "invalid action id",
+                                    "action buffer overflow"};
+        return fail("device error %d: %s", h, h > 0 && h < 7 ? msg[h] : "unknown");
+    }
+
+    // env 0's record (k_get_env0): 64-B header (group sizes, error word, done), then per group
+    // ids | rewards | positions | alive, info_rows rows each
+    static constexpr size_t kInfoRowBytes = 4 + 4 + 8 + 1;
+    size_t info_region() const { return ((info_rows * kInfoRowBytes) + 15) & ~(size_t)15; }
+    size_t info_off(int g, int what) const {
+        const size_t base = 64 + (size_t)g * info_region();
+        if (what == kGetId) return base;
+        if (what == kGetReward) return base + info_rows * 4;
+        if (what == kGetPos) return base + info_rows * 8;
+        return base + info_rows * 16;                                // kGetAlive
+    }
+    const int32_t* info_hdr() const { return reinterpret_cast<const int32_t*>(pin_info.p); }
+
+    // Queue the record's launch and its one copy to pinned memory (no sync).
+    int queue_info() {
+        const int G = n_groups();
+        size_t rows = 1;
+        for (int g = 0; g < G; g++) rows = std::max(rows, (size_t)std::max(group_ub[g], 1));
+        try {
+            if (rows > info_rows) info_rows = rows;
+            st_info.ensure(64 + (size_t)G * info_region());
+            pin_info.ensure(64 + (size_t)G * info_region());
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        MFX_HIP(launch_get_env0(d_gp, s, st_info.p, (int)info_rows, stream));
+        MFX_HIP(hipMemcpyAsync(pin_info.p, st_info.p, 64 + (size_t)G * info_region(), hipMemcpyDeviceToHost, stream));
+        return 0;
+    }
+
+    // after the sync that follows queue_info: this epoch's group sizes and info are on the host
+    int take_info() {
+        for (int g = 0; g < n_groups(); g++) hn[g] = info_hdr()[g];
+        n_ep = info_ep = epoch;
+        return report_err(info_hdr()[kMaxGroups]);
+    }
+
+    int ensure_info() {
+        if (info_ep == epoch) return 0;
+        MFX_CHECK(queue_info());
         MFX_HIP(hipStreamSynchronize(stream));
-        return n;
+        return take_info();
+    }
+    int ensure_counts() { return n_ep == epoch ? 0 : ensure_info(); }
+
+    int num_env0(int g) {
+        if (!allocated) return 0;
+        if (ensure_counts() != 0) return 0;
+        return hn[g];
+    }
+
+    size_t obs_off_view(int g) const { return (size_t)g * obs_rows * obs_row_bytes(); }
+    size_t obs_row_bytes() const {
+        size_t b = 0;
+        for (int g = 0; g < n_groups(); g++) {
+            const TypeParams& T = gp.type[g];
+            b = std::max(b, (size_t)4 * ((size_t)T.view_w * T.view_h * gp.n_ch + gp.feat_size[g]));
+        }
+        return (b + 15) & ~(size_t)15;
+    }
+
+    // views + features of every group of env 0 (and the info of the same epoch) in one transfer
+    int ensure_obs() {
+        if (obs_ep == epoch) return 0;
+        MFX_CHECK(ensure_counts());
+        const int G = n_groups();
+        int rowcap = 4;
+        for (int g = 0; g < G; g++) rowcap = std::max(rowcap, group_ub[g]);
+        rowcap = (rowcap + 3) & ~3;
+        size_t vmax = 0, fmax = 0;
+        for (int g = 0; g < G; g++) {
+            const TypeParams& T = gp.type[g];
+            vmax = std::max(vmax, (size_t)T.view_w * T.view_h * gp.n_ch);
+            fmax = std::max(fmax, (size_t)gp.feat_size[g]);
+        }
+        try {
+            obs_rows = std::max(obs_rows, (size_t)rowcap);
+            st_view.ensure((size_t)G * E * rowcap * vmax);
+            st_feat.ensure((size_t)G * E * rowcap * fmax);
+            pin_obs.ensure((size_t)G * obs_rows * obs_row_bytes());
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        for (int g = 0; g < G; g++) {
+            if (!hn[g]) continue;
+            const TypeParams& T = gp.type[g];
+            const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
+            float* dv = st_view.p + (size_t)g * E * rowcap * vmax;
+            float* df = st_feat.p + (size_t)g * E * rowcap * fmax;
+            MFX_CHECK(observe(g, dv, df, rowcap));
+            uint8_t* hv = pin_obs.p + obs_off_view(g);
+            MFX_HIP(hipMemcpyAsync(hv, dv, sizeof(float) * hn[g] * VF, hipMemcpyDeviceToHost, stream));
+            MFX_HIP(hipMemcpyAsync(hv + sizeof(float) * obs_rows * VF, df, sizeof(float) * hn[g] * F,
+                                   hipMemcpyDeviceToHost, stream));
+        }
+        MFX_CHECK(queue_info());                 // this epoch's ids (and the error word) ride along
+        MFX_HIP(hipStreamSynchronize(stream));
+        obs_ep = epoch;
+        return take_info();
     }
 
     // ------------------------------------------------------------------ batched device API
@@ -724,6 +850,7 @@ public:
         return 0;
     }
     int set_action(int g, const int* d_actions, int rowcap) {
+        touch();
         if (!allocated || g < 0 || g >= n_groups()) return fail("set_action: bad state or group");
         pending_ub += group_ub[g];
         try { ensure_capacity(0, pending_ub); } catch (const HipFailure& f) { return fail("%s", f.what()); }
@@ -731,6 +858,7 @@ public:
         return 0;
     }
     int step(int* d_done) {
+        touch();
         ro_prep_stale = true;
         if (!allocated) return fail("step before reset");
         MFX_CHECK(sync_cells());
@@ -745,6 +873,7 @@ public:
         return 0;
     }
     int clear_dead() {
+        touch();
         ro_prep_stale = true;
         if (!allocated) return fail("clear_dead before reset");
         MFX_HIP(launch_clear_dead(d_gp, s, stream));
@@ -892,6 +1021,7 @@ public:
     }
 
     int rollout_step(int n_steps) {
+        touch();
         if (!rollout_ready) return fail("rollout_step before rollout_init");
         if (walls_after_init) return fail("rollout: walls added after rollout_init are not part of the rollout's episodes");
         if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
@@ -971,40 +1101,79 @@ public:
     // ------------------------------------------------------------------ drop-in (env 0, host buffers)
     int host_observe(int g, float** bufs) {
         if (!allocated) return fail("get_observation before reset");
-        const int n = num_env0(g);
+        if (g < 0 || g >= n_groups()) return fail("get_observation: bad group %d", g);
+        MFX_CHECK(ensure_obs());
+        const int n = hn[g];
         if (n == 0) return 0;
         const TypeParams& T = gp.type[g];
         const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
-        const int rowcap = std::max(group_ub[g], 4);
-        st_view.ensure((size_t)E * rowcap * VF);
-        st_feat.ensure((size_t)E * rowcap * F);
-        MFX_CHECK(observe(g, st_view.p, st_feat.p, rowcap));
-        MFX_HIP(hipMemcpyAsync(bufs[0], st_view.p, sizeof(float) * n * VF, hipMemcpyDeviceToHost, stream));
-        MFX_HIP(hipMemcpyAsync(bufs[1], st_feat.p, sizeof(float) * n * F, hipMemcpyDeviceToHost, stream));
-        MFX_HIP(hipStreamSynchronize(stream));
-        return check_err();
+        const uint8_t* hv = pin_obs.p + obs_off_view(g);
+        memcpy(bufs[0], hv, sizeof(float) * n * VF);
+        memcpy(bufs[1], hv + sizeof(float) * obs_rows * VF, sizeof(float) * n * F);
+        return 0;
     }
+    // No sync: the actions go out of pinned memory (one region per group, reused once the previous
+    // copy from it has left), the launch is queued, device errors surface at the next cache fetch.
     int host_set_action(int g, const int* actions) {
         if (!allocated) return fail("set_action before reset");
+        if (g < 0 || g >= n_groups()) return fail("set_action: bad group %d", g);
         const int n = num_env0(g);
         const int rowcap = std::max(group_ub[g], 1);
-        st_i32.ensure((size_t)E * rowcap);
-        if (n) MFX_HIP(hipMemcpyAsync(st_i32.p, actions, sizeof(int) * n, hipMemcpyHostToDevice, stream));
-        MFX_CHECK(set_action(g, st_i32.p, rowcap));
-        MFX_HIP(hipStreamSynchronize(stream));
-        return check_err();
+        try {
+            st_i32.ensure((size_t)E * rowcap);
+            if (pin_act.n < (size_t)n_groups() * rowcap) {
+                MFX_HIP_THROW(hipStreamSynchronize(stream));            // no copy may be in flight
+                pin_act.ensure((size_t)n_groups() * rowcap);
+            }
+            if (!act_ev[g]) MFX_HIP_THROW(hipEventCreateWithFlags(&act_ev[g], hipEventDisableTiming));
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        const size_t stride = pin_act.n / n_groups();
+        int32_t* pa = pin_act.p + (size_t)g * stride;
+        MFX_HIP(hipEventSynchronize(act_ev[g]));
+        if (n) {
+            memcpy(pa, actions, sizeof(int) * n);
+            MFX_HIP(hipMemcpyAsync(st_i32.p, pa, sizeof(int) * n, hipMemcpyHostToDevice, stream));
+            MFX_HIP(hipEventRecord(act_ev[g], stream));
+        }
+        const int keep_n = n_ep == epoch;
+        MFX_CHECK(set_action(g, st_i32.p, rowcap));   // a state change: last_act feeds the features
+        if (keep_n) n_ep = epoch;                     // group sizes do not change
+        return 0;
     }
     int host_step(int* done) {
+        const int keep_n = n_ep == epoch;
+        (void)keep_n;
         MFX_CHECK(step(nullptr));
-        int32_t d = 0;
-        MFX_HIP(hipMemcpyAsync(&d, s.done, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        MFX_CHECK(queue_info());                   // done + rewards / alive / positions in one transfer
         MFX_HIP(hipStreamSynchronize(stream));
-        *done = d;
-        return check_err();
+        *done = info_hdr()[kMaxGroups + 1];
+        return take_info();
+    }
+    // clear_dead without a sync: with this epoch's alive flags at hand, the new group sizes are known.
+    int host_clear_dead() {
+        const int G = n_groups();
+        int nn[kMaxGroups] = {};
+        const bool known = allocated && info_ep == epoch && n_ep == epoch;
+        if (known)
+            for (int g = 0; g < G; g++) {
+                const uint8_t* al = pin_info.p + info_off(g, kGetAlive);
+                for (int i = 0; i < hn[g]; i++) nn[g] += al[i] != 0;
+            }
+        MFX_CHECK(clear_dead());
+        if (known) { for (int g = 0; g < G; g++) hn[g] = nn[g]; n_ep = epoch; }
+        return 0;
     }
     int host_get(int g, int what, void* out, size_t elem_bytes) {
+        if (g < 0 || g >= n_groups()) return fail("get: bad group %d", g);
         const int n = num_env0(g);
         if (n == 0) return 0;
+        if (what == kGetId || what == kGetReward || what == kGetPos || what == kGetAlive) {
+            MFX_CHECK(ensure_info());
+            memcpy(out, pin_info.p + info_off(g, what), elem_bytes * n);
+            return 0;
+        }
         const int rowcap = std::max(group_ub[g], 1);
         st_u8.ensure((size_t)E * rowcap * elem_bytes);
         MFX_CHECK(get(g, what, st_u8.p, rowcap));
@@ -1291,10 +1460,7 @@ MFX_API int gridworld_add_agents(void* game, int group, int n, const char* metho
                                  const int* dir) {
     MFX_GUARD(MFX_ENV(game)->add_agents(group, n, method, pos_x, pos_y, dir));
 }
-MFX_API int gridworld_clear_dead(void* game) {
-    BattleEngine* e = MFX_ENV(game);
-    MFX_GUARD(e->clear_dead() ? -1 : (hipStreamSynchronize(e->stream) == hipSuccess ? 0 : -1));
-}
+MFX_API int gridworld_clear_dead(void* game) { MFX_GUARD(MFX_ENV(game)->host_clear_dead()); }
 MFX_API int gridworld_set_goal(void* game, int group, const char* method, const int* linear_buffer) {
     (void)linear_buffer;
     MFX_GUARD(MFX_ENV(game)->set_goal(group, method));

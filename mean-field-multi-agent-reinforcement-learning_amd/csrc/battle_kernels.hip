@@ -2242,6 +2242,44 @@ __global__ void __launch_bounds__(256) k_clear_dead(const GameParams* __restrict
     if (TID == 0) s.idx_mark[blockIdx.x] = s.id_counter[blockIdx.x];
 }
 
+// The drop-in host cache's record of env 0 (one workgroup): header [group sizes (kMaxGroups),
+// device error word, done flag, ...] (64 B), then per group ids i32 | reward f32 | pos 2 x i32 |
+// alive u8, `rows` rows each (region rounded to 16 B) -- everything the reference's getters read
+// after a step, copied to the host in ONE transfer.
+__global__ void __launch_bounds__(256) k_get_env0(const GameParams* __restrict__ gp, State s, uint8_t* __restrict__ out,
+                                                  int rows) {
+    const int G = gp->n_groups;
+    EnvView v = global_view(s, 0, G);
+    int32_t* hdr = reinterpret_cast<int32_t*>(out);
+    if (TID < kMaxGroups) hdr[TID] = TID < G ? v.grp_n[TID] : 0;
+    if (TID == kMaxGroups) hdr[kMaxGroups] = *s.err;
+    if (TID == kMaxGroups + 1) hdr[kMaxGroups + 1] = s.done[0];
+    const size_t region = ((size_t)rows * 17 + 15) & ~(size_t)15;
+    for (int g = 0; g < G; ++g) {
+        const int n = min(v.grp_n[g], rows);
+        uint8_t* b = out + 64 + (size_t)g * region;
+        int32_t* ids = reinterpret_cast<int32_t*>(b);
+        float* rew = reinterpret_cast<float*>(b + (size_t)rows * 4);
+        int32_t* pos = reinterpret_cast<int32_t*>(b + (size_t)rows * 8);
+        uint8_t* alive = b + (size_t)rows * 16;
+        const uint16_t* gi = v.grp_ids + g * v.cap;
+        for (int i = TID; i < n; i += blockDim.x) {
+            const int id = gi[i];
+            const uint32_t p = v.xy[id];
+            ids[i] = id;
+            rew[i] = v.next_r[id] + v.grp_reward[g];
+            pos[2 * i] = (int)(p & 0xFFFF);
+            pos[2 * i + 1] = (int)(p >> 16);
+            alive[i] = !meta_dead(v.meta[id]);
+        }
+    }
+}
+
+hipError_t launch_get_env0(const GameParams* d_gp, const State& s, uint8_t* d_out, int rows, hipStream_t st) {
+    k_get_env0<<<1, 256, 0, st>>>(d_gp, s, d_out, rows);
+    return hipGetLastError();
+}
+
 // ==================================================================================
 //  getters: reward (GridWorld.cc:760-770) and info num/id/pos/alive (GridWorld.cc:786-807)
 // ==================================================================================

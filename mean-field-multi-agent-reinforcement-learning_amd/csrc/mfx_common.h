@@ -59,6 +59,20 @@ struct HipFailure : std::runtime_error {
 namespace mfx {
 
 template <class T>
+struct PinBuf {                    // grow-only pinned host buffer (async DMA target / source)
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t want) {
+        if (want <= n) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        MFX_HIP_THROW(hipHostMalloc((void**)&p, sizeof(T) * want, hipHostMallocDefault));
+        n = want;
+    }
+    ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+
+template <class T>
 struct DevBuf {                    // grow-only device buffer
     T* p = nullptr;
     size_t n = 0;

@@ -1,0 +1,65 @@
+"""The drop-in single-env path (magent.GridWorld over the HIP engine, host numpy buffers, the
+reference's own call sequence) timed exactly like bench.py's cpu_baseline: env calls only, the numpy
+rush policy outside the clock.  Prints agent-steps/s for the HIP drop-in and, when built, the C oracle.
+
+    python scripts/bench_dropin.py [--map 64 --agents 256 --seconds 5]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mean-field-multi-agent-reinforcement-learning_amd", "python"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (binds the engine to torch's HIP runtime)
+import battle_driver as bd  # noqa: E402
+import magent  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--map", type=int, default=64)
+ap.add_argument("--agents", type=int, default=256)
+ap.add_argument("--seconds", type=float, default=5.0)
+a = ap.parse_args()
+
+
+def run(lib_path):
+    env = magent.GridWorld("battle", map_size=a.map, lib=magent.load_library(lib_path))
+    h = env.get_handles()
+    _, v2a = env.get_view2attack(h[0])
+    left, right = bd.block_positions(a.map, a.agents // 2)
+    rng = np.random.RandomState(0)
+    clock, steps_n, calls = 0.0, 0, 0
+    while clock < a.seconds:
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        done, k = False, 0
+        while not done and k < 400 and clock < a.seconds:
+            t = time.perf_counter()
+            obs = [env.get_observation(h[g]) for g in range(2)]
+            for g in range(2):
+                env.get_agent_id(h[g])
+            clock += time.perf_counter() - t
+            acts = [bd.rush_policy(obs[g][0], obs[g][1], rng, v2a, 13, 21) for g in range(2)]
+            t = time.perf_counter()
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                env.get_reward(h[g])
+                env.get_alive(h[g])
+            env.clear_dead()
+            clock += time.perf_counter() - t
+            steps_n += len(obs[0][0]) + len(obs[1][0])
+            k += 1
+    return steps_n / clock
+
+
+out = {"map": a.map, "agents": a.agents, "hip_dropin": run(None)}
+oracle = os.path.join(REPO, "oracle", "build", "libbattle_oracle.so")
+if os.path.exists(oracle):
+    out["c_oracle_1thread"] = run(oracle)
+print(json.dumps(out))
