@@ -1363,6 +1363,13 @@ __host__ __device__ inline size_t big_scratch_bytes(int acap, int cap, bool full
     return big_region_bytes(acap, cap, full) + 16;
 }
 
+// k_step's LDS-mode step scratch: the wave-team forms (ParScratch) or the workgroup forms
+// (BigScratch, compact), at the same base
+__host__ __device__ inline size_t step_par_bytes(int acap, int cap) {
+    const size_t a = par_scratch_bytes(acap, cap), b = big_scratch_bytes(acap, cap, false);
+    return a > b ? a : b;
+}
+
 __device__ __forceinline__ BigScratch carve_big(char* base, int acap, int cap, bool full = true) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t m = (size_t)(acap > cap ? acap : cap) + 1;
@@ -2159,6 +2166,7 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     uint32_t* atk = s.atk + (size_t)e * s.acap;
     uint32_t* mov = s.mov + (size_t)e * s.acap;
     uint32_t* sorted = sort_scratch + (size_t)e * s.acap;
+    char* par_base = nullptr;              // LDS mode: the parallel step's scratch (ParScratch / BigScratch)
     if (lds) {
         size_t off = step_sm_bytes(G);
         auto carve = [&](size_t bytes) { char* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
@@ -2171,6 +2179,7 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
         uint32_t* latk = reinterpret_cast<uint32_t*>(carve((size_t)n_atk * 4));
         uint32_t* lmov = reinterpret_cast<uint32_t*>(carve((size_t)n_mov * 4));
         uint32_t* lsort = reinterpret_cast<uint32_t*>(carve((size_t)(gp.large_map ? n_mov : 0) * 4));
+        par_base = gp.par_step ? carve(step_par_bytes(s.acap, s.cap)) : nullptr;
         for (int i = TID; i < s.cells_n; i += blockDim.x) v.cells[i] = gv.cells[i];
         for (int i = TID; i < nid; i += blockDim.x) {
             v.xy[i] = gv.xy[i]; v.hp[i] = gv.hp[i]; v.next_r[i] = gv.next_r[i];
@@ -2185,8 +2194,10 @@ __global__ void __launch_bounds__(256) k_step(const GameParams* __restrict__ gpp
     int done = 0;
     load_serial_types(gp, sm);
     int32_t* ev = (gp.record_events && e == 0) ? s.ev : nullptr;
-    step_env_core<false, kDsl>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, false, ParScratch{}, nid, ev,
-                               kDsl ? s.idx_mark[e] : 0);
+    const ParScratch ps = par_base ? carve_par(par_base, s.acap, s.cap) : ParScratch{};
+    const BigScratch bs = par_base ? carve_big(par_base, s.acap, s.cap, false) : BigScratch{};
+    step_env_core<false, kDsl>(gp, s, v, atk, n_atk, mov, n_mov, sorted, rng, sm, done, par_base != nullptr, ps, nid,
+                               ev, kDsl ? s.idx_mark[e] : 0, par_base ? &bs : nullptr);
     if (lds) {
         for (int i = TID; i < s.cells_n; i += blockDim.x) gv.cells[i] = v.cells[i];
         for (int i = TID; i < nid; i += blockDim.x) {
@@ -3039,10 +3050,10 @@ size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cel
     return b;
 }
 
-size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap) {
+size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap, int cap) {
     auto r16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     return r16((size_t)cells_n * 2) + 4 * r16((size_t)n_ids * 4) + r16(n_ids) + 2 * r16((size_t)acap * 4) +
-           (gp.large_map ? r16((size_t)acap * 4) : 0);
+           (gp.large_map ? r16((size_t)acap * 4) : 0) + (gp.par_step ? r16(step_par_bytes(acap, cap)) : 0);
 }
 
 hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st) {
@@ -3482,7 +3493,7 @@ hipError_t launch_set_action(const GameParams* d_gp, const State& s, int g, cons
 
 hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State& s, int max_ids,
                        uint32_t* d_sort_scratch, hipStream_t st) {
-    const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap) + step_sm_bytes(gp.n_groups);
+    const size_t smem = step_smem_bytes(gp, s.cells_n, max_ids, s.acap, s.cap) + step_sm_bytes(gp.n_groups);
     const int lds = smem <= 96 * 1024;
     const size_t big = big_step_smem_bytes(gp, s.cap, s.acap, false);
     if (!lds && !gp.dsl && gp.par_step && !gp.record_events && big <= 160 * 1024) {
