@@ -155,18 +155,25 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    red = None
     for k in range(args.steps):
         ev[k][0].record(stream)
         eng.rollout_step(1)
         ev[k][1].record(stream)
-        if world > 1:          # episode statistics -> RCCL all-reduce (the only collective)
+        # episode statistics -> RCCL all-reduce, once per episode batch (an episode cap of steps) and at
+        # the end of the timed window: the only collective
+        if world > 1 and ((k + 1) % args.max_steps == 0 or k == args.steps - 1):
             eng.rollout_copy("stats", stats_buf)
-            reduce_stats(stats_buf.view(E, 4))
+            red = reduce_stats(stats_buf.view(E, 4))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     a1 = agent_steps()
+    if red is None:                  # one rank: the same statistics, reduced after the clock
+        eng.rollout_copy("stats", stats_buf)
+        red = reduce_stats(stats_buf.view(E, 4))
+    red = red.tolist()
     kernel_ms = sum(s.elapsed_time(e) for s, e in ev) / args.steps
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
@@ -202,6 +209,8 @@ def main():
                          "kernel": "k_observe_items+k_rollout_big" if big else "k_rollout", "kernel_ms": kernel_ms,
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch},
             "cpu_baseline": None,
+            "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],
+                         "kills": red[3], "note": "all ranks, since rollout_init (RCCL all-reduce per episode batch)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = run_cpu_baseline_subprocess(args.cpu_seconds, args.map, args.agents)
