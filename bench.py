@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--backend", default="nccl", help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.envs is None:
         a.envs = 16384 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
@@ -123,9 +124,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())     # (rehearsals: several ranks on one GPU)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":           # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:                                # rehearsal of the N-rank flow without RCCL
+            dist.init_process_group(args.backend)
     stream = torch.cuda.current_stream()
 
     eng = BattleBatch(args.map, args.envs, stream=stream)

@@ -951,6 +951,7 @@ public:
 
     // Reset image, work queue and persistent grid for the current capacity.
     int rollout_plan() {
+        ro_prep_stale = true;                    // the large-env observation inputs follow the new plan
         try {
             ro_work.ensure(2);
             MFX_HIP_THROW(hipMemsetAsync(ro_work.p, 0, 2 * sizeof(int32_t), stream));
