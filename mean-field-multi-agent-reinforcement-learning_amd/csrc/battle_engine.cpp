@@ -178,12 +178,24 @@ public:
     // k_observe_items slots, leaving room for the other stream's step.  Measured at 256x256 / 4096
     // agents, 1024 envs (profiles/r01_big_sweeps.txt): 2 streams / 1/3 grid / 64-agent items best.
     static constexpr int kBigSplit = 2, kItemGridDiv = 3, kItemRows = 64;
+    static constexpr bool kPipeDefault = false;   // measured slower than the fused step
+    static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
     hipStream_t ro_str[kMaxSplit] = {};
     hipEvent_t ro_ev[kMaxSplit + 1] = {};
     State ro_sub_s[kMaxSplit];
     RolloutArgs ro_sub_ra[kMaxSplit];
     DevBuf<RolloutCtx> ro_sub_ctx;
+    // observation/step pipeline (LDS-sized envs): k_rollout_obs on ro_str[0] observes every env
+    // from one copy of the per-env state while k_rollout<.., kSplit> steps the same envs from it
+    // and writes the other copy (tw); the copies trade places after every launch.
+    bool ro_pipe = false;
+    State tw{};                              // the other copy (the kTwin fields below)
+    int tw_cap = -1, tw_E = -1;
+    int ro_par = 0;                          // 0: s is ro_pipe_ctx[0].s
+    int ro_obs_grid = 0;
+    DevBuf<RolloutCtx> ro_pipe_ctx;          // [2]: {s, ra, tw} and {tw, ra, s} as planned
+    RolloutCtx ro_pipe_host[2] = {};
 
     ~BattleEngine() {
         for (auto& x : act_ev) if (x) (void)hipEventDestroy(x);
@@ -237,7 +249,38 @@ public:
                         (void*)d_err})
             if (p) (void)hipFree(p);
         s = State{}; d_sort = nullptr; d_gp = nullptr; d_err = nullptr; allocated = false;
+        free_twin();
     }
+
+    // The per-env fields k_rollout reads and writes back (the pipeline keeps two copies of them).
+    template <class F> static void twin_fields(State& a, State& b, F&& f) {
+        f(a.xy, b.xy); f(a.hp, b.hp); f(a.next_r, b.next_r); f(a.last_r, b.last_r); f(a.last_act, b.last_act);
+        f(a.op_obj, b.op_obj); f(a.meta, b.meta); f(a.grp_ids, b.grp_ids); f(a.grp_n, b.grp_n);
+        f(a.grp_dead, b.grp_dead); f(a.grp_reward, b.grp_reward); f(a.id_counter, b.id_counter); f(a.rng, b.rng);
+    }
+    void free_twin() {
+        State none{};
+        twin_fields(tw, none, [](auto& p, auto&) { if (p) (void)hipFree(p); p = nullptr; });
+        tw_cap = tw_E = -1;
+        ro_par = 0;
+    }
+    void alloc_twin() {
+        if (tw_cap == s.cap && tw_E == E) return;
+        free_twin();
+        const size_t c = (size_t)s.cap, G = (size_t)n_groups();
+        alloc(tw.xy, E * c); alloc(tw.hp, E * c); alloc(tw.next_r, E * c); alloc(tw.last_r, E * c);
+        alloc(tw.last_act, E * c); alloc(tw.op_obj, E * c); alloc(tw.meta, E * c); alloc(tw.grp_ids, E * G * c);
+        alloc(tw.grp_n, E * G); alloc(tw.grp_dead, E * G); alloc(tw.grp_reward, E * G); alloc(tw.id_counter, E);
+        alloc(tw.rng, E);
+        tw_cap = s.cap; tw_E = E;
+    }
+    // s with tw's copies of the twin fields
+    State twin_state() const {
+        State t = s, x = tw;
+        twin_fields(t, x, [](auto& a, auto& b) { a = b; });
+        return t;
+    }
+    void swap_twin() { twin_fields(s, tw, [](auto& a, auto& b) { std::swap(a, b); }); }
 
     int n_groups() const { return (int)group_types.size(); }
     AgentTypeSpec& gtype(int g) { return types.at(group_types.at(g)); }
@@ -953,8 +996,8 @@ public:
     int rollout_plan() {
         ro_prep_stale = true;                    // the large-env observation inputs follow the new plan
         try {
-            ro_work.ensure(2);
-            MFX_HIP_THROW(hipMemsetAsync(ro_work.p, 0, 2 * sizeof(int32_t), stream));
+            ro_work.ensure(4);                   // [0..1] k_rollout, [2..3] k_rollout_obs
+            MFX_HIP_THROW(hipMemsetAsync(ro_work.p, 0, 4 * sizeof(int32_t), stream));
             ro_image.ensure((rollout_reset_image_bytes(gp, s.cells_n, s.cap) + 15) / 16);
             // queue for the next launch: every env in class 0 in index order, other counts zero
             ro_cls_cnt.ensure(3 * 8); ro_cls_list.ensure((size_t)2 * 8 * E);
@@ -1008,11 +1051,29 @@ public:
                 MFX_HIP_THROW(hipMemcpyAsync(ro_sub_ctx.p, subs.data(), sizeof(RolloutCtx) * K, hipMemcpyHostToDevice,
                                              stream));
             } else {
-                MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, &ro_grid));
+                const char* pv = getenv("MFX_ROLLOUT_PIPE");
+                ro_pipe = pv ? atoi(pv) != 0 : kPipeDefault;
+                if (ro_pipe) {
+                    const char* a = getenv("MFX_PIPE_STEP_PER_CU");
+                    const char* b = getenv("MFX_PIPE_OBS_PER_CU");
+                    MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, 1, a ? atoi(a) : kPipeStepPerCu, &ro_grid));
+                    MFX_HIP_THROW(rollout_obs_grid(gp, s, ra.rowcap, b ? atoi(b) : kPipeObsPerCu, &ro_obs_grid));
+                    alloc_twin();
+                    ro_par = 0;
+                    ro_pipe_host[0].s = s; ro_pipe_host[0].ra = ra; ro_pipe_host[0].w = twin_state();
+                    ro_pipe_host[1].s = twin_state(); ro_pipe_host[1].ra = ra; ro_pipe_host[1].w = s;
+                    ro_pipe_ctx.ensure(2);
+                    MFX_HIP_THROW(hipMemcpyAsync(ro_pipe_ctx.p, ro_pipe_host, sizeof(ro_pipe_host), hipMemcpyHostToDevice,
+                                                 stream));
+                    if (!ro_str[0]) MFX_HIP_THROW(hipStreamCreateWithFlags(&ro_str[0], hipStreamNonBlocking));
+                    for (auto& x : ro_ev) if (!x) MFX_HIP_THROW(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+                } else {
+                    MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, 0, 0, &ro_grid));
+                }
             }
             ro_cap = s.cap;
             ro_ctx.ensure(1);
-            ro_ctx_host.s = s; ro_ctx_host.ra = ra;
+            ro_ctx_host.s = s; ro_ctx_host.ra = ra; ro_ctx_host.w = s;
             MFX_HIP_THROW(hipMemcpyAsync(ro_ctx.p, &ro_ctx_host, sizeof(RolloutCtx), hipMemcpyHostToDevice, stream));
             MFX_HIP_THROW(hipStreamSynchronize(stream));
         } catch (const HipFailure& f) {
@@ -1025,7 +1086,10 @@ public:
         touch();
         if (!rollout_ready) return fail("rollout_step before rollout_init");
         if (walls_after_init) return fail("rollout: walls added after rollout_init are not part of the rollout's episodes");
-        if (s.cap != ro_cap || memcmp(&ro_ctx_host.s, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
+        {
+            const State& planned = ro_pipe ? ro_pipe_host[ro_par].s : ro_ctx_host.s;
+            if (s.cap != ro_cap || memcmp(&planned, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
+        }
         if (ro_big) {
             MFX_CHECK(sync_cells());
             const int K = std::min(ro_split, E);
@@ -1061,9 +1125,28 @@ public:
             }
             return 0;
         }
+        if (ro_pipe) {
+            for (int i = 0; i < n_steps; i++) {
+                const RolloutCtx* c = ro_pipe_ctx.p + ro_par;
+                const int qp = (int)(ro_launch % 6);
+                MFX_HIP(hipEventRecord(ro_ev[kMaxSplit], stream));
+                MFX_HIP(hipStreamWaitEvent(ro_str[0], ro_ev[kMaxSplit], 0));
+                MFX_HIP(launch_rollout_obs(gp, d_gp, s, c, ra.rowcap, ra.work_sel, qp, ro_obs_grid, ro_str[0]));
+                MFX_HIP(launch_rollout(gp, d_gp, s, c, ra.rowcap, ra.step_index, ra.work_sel, qp, ro_grid, 1, stream));
+                MFX_HIP(hipEventRecord(ro_ev[0], ro_str[0]));
+                MFX_HIP(hipStreamWaitEvent(stream, ro_ev[0], 0));
+                swap_twin();                     // the written copy is the state now
+                ro_par ^= 1;
+                ro_launch++;
+                ra.step_index++;
+                ra.work_sel ^= 1;
+                cells_stale = true;
+            }
+            return 0;
+        }
         for (int i = 0; i < n_steps; i++) {
             MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
-                                   ro_grid, stream));
+                                   ro_grid, 0, stream));
             ro_launch++;
             ra.step_index++;
             ra.work_sel ^= 1;

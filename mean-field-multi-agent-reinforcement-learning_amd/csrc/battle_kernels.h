@@ -31,11 +31,16 @@ hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t
 hipError_t set_stamp_buffer(unsigned long long* d_buf);
 size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap, int rows);
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                          int rows, uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st);
+                          int rows, uint32_t step_index, int work_sel, int qphase, int grid, int split,
+                          hipStream_t st);
+size_t rollout_obs_smem_bytes(const GameParams& gp, int cells_n, int cap, int rows);
+hipError_t launch_rollout_obs(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                              int rows, int work_sel, int qphase, int grid, hipStream_t st);
+hipError_t rollout_obs_grid(const GameParams& gp, const State& s, int rows, int per_cu_want, int* grid);
 size_t big_step_smem_bytes(const GameParams& gp, int cap, int acap, bool rollout);
 hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                               uint32_t step_index, hipStream_t st);
-hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int* grid);
+hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int split, int per_cu_want, int* grid);
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap);
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
                               uint4* d_image, hipStream_t st);

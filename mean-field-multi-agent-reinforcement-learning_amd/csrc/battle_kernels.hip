@@ -2535,10 +2535,10 @@ constexpr int kScalarWords = 30;
 // order, so the prefetch waves must not have the write-back stores queued ahead of their loads.
 // The image's 16-B rows are numbered in LDS order: the cells (nc16 rows), then
 // [xy hp next_r last_r op_obj] (c4 = cap/4 rows each), [last_act] [meta] (c4/4 each), [grp_ids] (G*c4/2).
-constexpr int kPfLanes = 192;                     // waves 0-2
+constexpr int kPfLanes = MFX_ROLLOUT_THREADS - 64; // every wave but the last
 constexpr int kPfSlots = 5;
 constexpr int kPfRows = kPfSlots * kPfLanes;
-constexpr int kWbWave = 3;                        // the write-back wave
+constexpr int kWbWave = MFX_ROLLOUT_THREADS / 64 - 1;   // the write-back wave
 
 __host__ __device__ inline int image_small_rows(int c4, int G) { return 5 * c4 + 2 * (c4 >> 2) + G * (c4 >> 1); }
 
@@ -2806,10 +2806,38 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
     MFX_TSTAMP(kW, 8);
 }
 
+// get_observation of every group of the env in LDS (after obs_prologue + obs_minimap): rows of
+// env e in ra.view / ra.feat.
+template <bool kB>
+__device__ __forceinline__ void rollout_observe_groups(const GameParams& gp, const RolloutArgs& ra, const EnvView& v,
+                                                       const ObsSmem& osm, int e) {
+    for (int g = 0; g < gp.n_groups; ++g) {
+        const TypeParams& T = gp.type[g];
+        const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
+        float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
+        float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
+        const int n = min(v.grp_n[g], ra.rowcap);
+        if (kB) {
+            obs_agent_records(gp, v, osm, g, n);
+            __syncthreads();
+#ifndef MFX_DIAG_NO_OBS                              // diagnostic builds only: everything but the stream
+            obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
+#endif
+            __syncthreads();                   // the records are rebuilt for the next group
+        } else {
+            obs_prologue(gp, osm, g);
+            __syncthreads();
+            for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
+        }
+    }
+}
+
 // One launch = one training-loop step for every env.  Persistent workgroups: the grid is what
 // fits on the chip at once, and each workgroup takes envs from a work queue, keeping env e in LDS
 // while the next env's image is already in flight into registers.
-template <bool kB, bool kPf>
+// kSplit: the step half of the observation/step pipeline -- no observation, and env e is written
+// back to ctx->w instead of ctx->s.
+template <bool kB, bool kPf, bool kSplit>
 __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollout(const GameParams* __restrict__ gpp,
                                                                  const RolloutCtx* __restrict__ ctx,
                                                                  uint32_t step_index, int work_sel, int qphase) {
@@ -2818,6 +2846,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
     __shared__ int misc[8];                  // 0 n_atk, 1 n_mov, 3 episode end, 4 done, 5-7 queue hand-off
     __shared__ int32_t n_before[kMaxGroups];
     __shared__ PfTable pt;
+    __shared__ PfTable ptw;                  // kSplit: the write-back copy's addresses
     __shared__ int qpre[kOrderClasses + 1], qtmp[kOrderClasses];
     __shared__ int wg_env[kQueueBuf];
     __shared__ uint8_t wg_cls[kQueueBuf];
@@ -2856,6 +2885,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         }
         load_serial_types(gp, sm);
         pf_table_init(pt, s, ra, G);
+        if (kSplit) pf_table_init(ptw, kconst(ctx).w, ra, G);
         __syncthreads();
         e = misc[5]; en = misc[6];
         if (TID == 0) o = misc[7];
@@ -2918,28 +2948,12 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
             g = atomicAdd(ra.work + work_sel, 1);
         }
         MFX_STAMP(1);
-        // ---------------- get_observation for every group
-        obs_prologue(gp, osm, 0);
-        obs_minimap<kB>(gp, v, osm, 0);              // one view size for every group (rollout_plan)
-        MFX_STAMP(2);
-        for (int g = 0; g < G; ++g) {
-            const TypeParams& T = gp.type[g];
-            const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
-            float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
-            float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
-            const int n = min(v.grp_n[g], ra.rowcap);
-            if (kB) {
-                obs_agent_records(gp, v, osm, g, n);
-                __syncthreads();
-#ifndef MFX_DIAG_NO_OBS                              // diagnostic builds only: everything but the stream
-                obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
-#endif
-                __syncthreads();               // the records are rebuilt for the next group
-            } else {
-                obs_prologue(gp, osm, g);
-                __syncthreads();
-                for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
-            }
+        // ---------------- get_observation for every group (k_rollout_obs in the pipeline)
+        if (!kSplit) {
+            obs_prologue(gp, osm, 0);
+            obs_minimap<kB>(gp, v, osm, 0);          // one view size for every group (rollout_plan)
+            MFX_STAMP(2);
+            rollout_observe_groups<kB>(gp, ra, v, osm, e);
         }
         __syncthreads();                       // the scratch region changes hands
         MFX_STAMP(3);
@@ -3013,7 +3027,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         // ---------------- write the env back (wave kWbWave only, see EnvPrefetch)
         if ((TID >> 6) == kWbWave) {
             const int lane = TID & 63;
-            const EnvView gv = global_view(s, e, G);   // cells: rebuilt at the next install
+            const EnvView gv = global_view(kSplit ? kconst(ctx).w : s, e, G);   // cells: rebuilt at the next install
             const int idc = sc.id_counter;
             const size_t n4 = ((size_t)idc + 3) & ~(size_t)3, n16 = ((size_t)idc + 15) & ~(size_t)15;
             wcopy16(gv.xy, v.xy, n4 * 4, lane);
@@ -3026,7 +3040,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
             for (int g = 0; g < G; ++g)
                 wcopy16(gv.grp_ids + g * cap, v.grp_ids + g * cap, (((size_t)v.grp_n[g] + 7) & ~(size_t)7) * 2, lane);
             if (lane < kScalarWords) {
-                g_u32* p = scalar_addr(pt, e, lane);
+                g_u32* p = scalar_addr(kSplit ? ptw : pt, e, lane);
                 if (p) *p = reinterpret_cast<const uint32_t*>(&sc)[lane];
             }
             if (lane == 0) { s.n_atk[e] = 0; s.n_mov[e] = 0; s.done[e] = misc[4]; }
@@ -3038,6 +3052,82 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
     }
     }
     if (TID == 0 && wg_n) queue_flush(kconst(ctx).ra, wg_env, wg_cls, wg_n, qphase, qtmp);
+}
+
+#ifndef MFX_OBS_OCC
+#define MFX_OBS_OCC 8              // k_rollout_obs: <= 64 VGPRs, so it fits beside k_rollout's waves
+#endif
+// The observation half of the pipeline: get_observation of every env of the launch from the
+// state before the step (ctx->s), beside k_rollout<.., kSplit> which steps the same envs from the
+// same copy and writes the other.  Persistent workgroups on their own counter (RolloutArgs::work
+// [2 + sel]) over the same heaviest-first queue; env e+1's image is in flight into registers
+// while env e is observed.  LDS: the env image, then the observation scratch.
+template <bool kB, bool kPf>
+__global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_OBS_OCC) k_rollout_obs(const GameParams* __restrict__ gpp,
+                                                                                 const RolloutCtx* __restrict__ ctx,
+                                                                                 int work_sel, int qphase) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ EnvScalars sc;
+    __shared__ int misc[4];                  // 0-1 queue hand-off
+    __shared__ PfTable pt;
+    __shared__ int qpre[kOrderClasses + 1];
+    int e, en;
+    EnvPrefetch pf;
+#pragma unroll
+    for (int j = 0; j < kPfSlots; ++j) pf.r[j] = make_uint4(0, 0, 0, 0);
+    pf.w = 0;
+    {
+        const GameParams& gp = kconst(gpp);
+        const State& s = kconst(ctx).s;
+        const RolloutArgs& ra = kconst(ctx).ra;
+        const int G = gp.n_groups, c4 = s.cap >> 2, sh = __ffs(c4) - 1;
+        const int nc16 = s.cells_n >> 3, nrows = nc16 + image_small_rows(c4, G);
+        if (TID == 0) {
+            if (blockIdx.x == 0) ra.work[2 + (work_sel ^ 1)] = 0;
+            int acc = 0;
+            for (int c = 0; c < kOrderClasses; ++c) { qpre[c] = acc; acc += ra.cls_cnt[(qphase % 3) * kOrderClasses + c]; }
+            qpre[kOrderClasses] = acc;
+            for (int k = 0; k < 2; ++k) misc[k] = queue_env(ra, qpre, atomicAdd(ra.work + 2 + work_sel, 1), s.E, qphase);
+        }
+        pf_table_init(pt, s, ra, G);
+        __syncthreads();
+        e = misc[0]; en = misc[1];
+        if (kPf && e < s.E) pf_issue(pf, pt, s, e, nrows, nc16, sh, c4);
+    }
+    while (true) {
+        const GameParams& gp = kconst(gpp);
+        const State& s = kconst(ctx).s;
+        const RolloutArgs& ra = kconst(ctx).ra;
+        if (e >= s.E) break;
+        const int G = gp.n_groups, cap = s.cap;
+        EnvView v = carve_env(smem, s.cells_n, cap, G);
+        v.grp_n = sc.grp_n; v.grp_dead = sc.grp_dead; v.grp_reward = sc.grp_reward;
+        size_t soff = env_image_bytes(s.cells_n, cap, G);
+        ObsSmem osm = carve_obs(smem, gp, 0, cap, ra.rowcap, obs_stage_floats(gp, 0, kB, blockDim.x), kB, soff);
+        if (!kB) osm.info = nullptr;
+        const int c4 = cap >> 2, sh = __ffs(c4) - 1;
+        const int nc16 = s.cells_n >> 3, nrows = nc16 + image_small_rows(c4, G);
+        if (kPf) pf_install(pf, smem, sc, nrows);
+        else install_sync(s, pt, e, G, v, sc);
+        __syncthreads();
+        for (int q = 0; q < G; ++q) {           // the listed agents onto the walls-only cells
+            const int nq = sc.grp_n[q];
+            for (int i = TID; i < nq; i += blockDim.x) {
+                const int id = v.grp_ids[q * cap + i];
+                const uint32_t p = v.xy[id];
+                if (!meta_dead(v.meta[id])) v.cells[(p >> 16) * gp.W + (p & 0xFFFF)] = (uint16_t)id;
+            }
+        }
+        if (TID == 0) misc[0] = queue_env(ra, qpre, atomicAdd(ra.work + 2 + work_sel, 1), s.E, qphase);
+        __syncthreads();
+        if (kPf && en < s.E) pf_issue(pf, pt, s, en, nrows, nc16, sh, c4);
+        obs_prologue(gp, osm, 0);
+        obs_minimap<kB>(gp, v, osm, 0);
+        rollout_observe_groups<kB>(gp, ra, v, osm, e);
+        __syncthreads();                        // the image and the hand-off change hands
+        e = en;
+        en = misc[0];
+    }
 }
 
 // ==================================================================================
@@ -3538,36 +3628,81 @@ static bool rollout_prefetch_ok(const GameParams& gp, const State& s) {
 }
 
 template <class F>
-static hipError_t with_rollout_kernel(const GameParams& gp, const State& s, F&& f) {
+static hipError_t with_rollout_kernel(const GameParams& gp, const State& s, bool split, F&& f) {
     if (is_battle_shape(gp)) {
-        if (rollout_prefetch_ok(gp, s)) return f(k_rollout<true, true>);
-        return f(k_rollout<true, false>);
+        if (rollout_prefetch_ok(gp, s)) return split ? f(k_rollout<true, true, true>) : f(k_rollout<true, true, false>);
+        return split ? f(k_rollout<true, false, true>) : f(k_rollout<true, false, false>);
     }
-    return f(k_rollout<false, false>);
+    return split ? f(k_rollout<false, false, true>) : f(k_rollout<false, false, false>);
+}
+
+template <class F>
+static hipError_t with_rollout_obs_kernel(const GameParams& gp, const State& s, F&& f) {
+    if (is_battle_shape(gp)) {
+        if (rollout_prefetch_ok(gp, s)) return f(k_rollout_obs<true, true>);
+        return f(k_rollout_obs<true, false>);
+    }
+    return f(k_rollout_obs<false, false>);
 }
 
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                          int rows, uint32_t step_index, int work_sel, int qphase, int grid, hipStream_t st) {
+                          int rows, uint32_t step_index, int work_sel, int qphase, int grid, int split,
+                          hipStream_t st) {
     const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rows);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
-    return with_rollout_kernel(gp, s, [&](auto kern) {
+    return with_rollout_kernel(gp, s, split != 0, [&](auto kern) {
         kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel, qphase);
         return hipGetLastError();
     });
 }
 
+// k_rollout_obs: the env image and the observation scratch
+size_t rollout_obs_smem_bytes(const GameParams& gp, int cells_n, int cap, int rows) {
+    const bool kB = is_battle_shape(gp);
+    return env_image_bytes(cells_n, cap, gp.n_groups) +
+           obs_smem_core(gp, 0, cap, rows, obs_stage_floats(gp, 0, kB, MFX_ROLLOUT_THREADS), kB);
+}
+
+hipError_t launch_rollout_obs(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                              int rows, int work_sel, int qphase, int grid, hipStream_t st) {
+    const size_t smem = rollout_obs_smem_bytes(gp, s.cells_n, s.cap, rows);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    return with_rollout_obs_kernel(gp, s, [&](auto kern) {
+        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, work_sel, qphase);
+        return hipGetLastError();
+    });
+}
+
 // Persistent grid of k_rollout: every workgroup that can be resident at once (more is harmless --
-// the extra ones find the queue empty -- fewer would idle CUs).
-hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int* grid) {
+// the extra ones find the queue empty -- fewer would idle CUs).  per_cu > 0: that many per CU
+// instead (the pipeline shares the CUs between k_rollout and k_rollout_obs).
+hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int split, int per_cu_want, int* grid) {
     const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rows);
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t err = hipGetDevice(&dev);
     if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (err != hipSuccess) return err;
-    err = with_rollout_kernel(gp, s, [&](auto kern) {
+    err = with_rollout_kernel(gp, s, split != 0, [&](auto kern) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, MFX_ROLLOUT_THREADS, smem);
     });
     if (err != hipSuccess) return err;
+    if (per_cu_want > 0 && per_cu_want < per_cu) per_cu = per_cu_want;
+    const long long want = (long long)cus * (per_cu > 0 ? per_cu : 1);
+    *grid = (int)(want < s.E ? want : s.E);
+    return hipSuccess;
+}
+
+hipError_t rollout_obs_grid(const GameParams& gp, const State& s, int rows, int per_cu_want, int* grid) {
+    const size_t smem = rollout_obs_smem_bytes(gp, s.cells_n, s.cap, rows);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (err != hipSuccess) return err;
+    err = with_rollout_obs_kernel(gp, s, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, MFX_ROLLOUT_THREADS, smem);
+    });
+    if (err != hipSuccess) return err;
+    if (per_cu_want > 0 && per_cu_want < per_cu) per_cu = per_cu_want;
     const long long want = (long long)cus * (per_cu > 0 ? per_cu : 1);
     *grid = (int)(want < s.E ? want : s.E);
     return hipSuccess;

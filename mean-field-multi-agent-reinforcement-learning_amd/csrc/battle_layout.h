@@ -186,9 +186,14 @@ struct RolloutArgs {
 
 // Everything k_rollout reads besides GameParams, resident in HBM (uploaded when it changes); the
 // kernel re-reads it per env through scalar loads instead of pinning ~80 SGPRs for the launch.
+// s: the state a launch reads; w: where k_rollout writes each env back.  The fused step has
+// w == s; the observation/step pipeline (k_rollout_obs beside k_rollout<.., kSplit>) reads one
+// copy of the per-env state and writes the other, so that both kernels of a launch see the state
+// before the step.
 struct RolloutCtx {
     State s;
     RolloutArgs ra;
+    State w;
 };
 
 // meta helpers

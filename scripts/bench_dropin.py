@@ -22,16 +22,30 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--map", type=int, default=64)
 ap.add_argument("--agents", type=int, default=256)
 ap.add_argument("--seconds", type=float, default=5.0)
+ap.add_argument("--calls", action="store_true", help="also report the time per call kind (us per step)")
 a = ap.parse_args()
 
 
-def run(lib_path):
+class Clock:
+    """Per-call-kind accumulator: clock.t(kind, fn, *args) times one env call."""
+    def __init__(self):
+        self.acc = {}
+
+    def t(self, kind, fn, *args):
+        t0 = time.perf_counter()
+        r = fn(*args)
+        self.acc[kind] = self.acc.get(kind, 0.0) + time.perf_counter() - t0
+        return r
+
+
+def run(lib_path, per_call=None):
+    ck = Clock()
     env = magent.GridWorld("battle", map_size=a.map, lib=magent.load_library(lib_path))
     h = env.get_handles()
     _, v2a = env.get_view2attack(h[0])
     left, right = bd.block_positions(a.map, a.agents // 2)
     rng = np.random.RandomState(0)
-    clock, steps_n, calls = 0.0, 0, 0
+    clock, steps_n, n_steps = 0.0, 0, 0
     while clock < a.seconds:
         env.reset()
         env.add_agents(h[0], method="custom", pos=left)
@@ -39,27 +53,33 @@ def run(lib_path):
         done, k = False, 0
         while not done and k < 400 and clock < a.seconds:
             t = time.perf_counter()
-            obs = [env.get_observation(h[g]) for g in range(2)]
+            obs = [ck.t("get_observation", env.get_observation, h[g]) for g in range(2)]
             for g in range(2):
-                env.get_agent_id(h[g])
+                ck.t("get_agent_id", env.get_agent_id, h[g])
             clock += time.perf_counter() - t
             acts = [bd.rush_policy(obs[g][0], obs[g][1], rng, v2a, 13, 21) for g in range(2)]
             t = time.perf_counter()
             for g in range(2):
-                env.set_action(h[g], acts[g])
-            done = env.step()
+                ck.t("set_action", env.set_action, h[g], acts[g])
+            done = ck.t("step", env.step)
             for g in range(2):
-                env.get_reward(h[g])
-                env.get_alive(h[g])
-            env.clear_dead()
+                ck.t("get_reward", env.get_reward, h[g])
+                ck.t("get_alive", env.get_alive, h[g])
+            ck.t("clear_dead", env.clear_dead)
             clock += time.perf_counter() - t
             steps_n += len(obs[0][0]) + len(obs[1][0])
             k += 1
+            n_steps += 1
+    if per_call is not None:
+        per_call.update({kk: round(1e6 * v / n_steps, 2) for kk, v in ck.acc.items()})
     return steps_n / clock
 
 
-out = {"map": a.map, "agents": a.agents, "hip_dropin": run(None)}
+pc_hip, pc_c = {}, {}
+out = {"map": a.map, "agents": a.agents, "hip_dropin": run(None, pc_hip)}
 oracle = os.path.join(REPO, "oracle", "build", "libbattle_oracle.so")
 if os.path.exists(oracle):
-    out["c_oracle_1thread"] = run(oracle)
+    out["c_oracle_1thread"] = run(oracle, pc_c)
+if a.calls:
+    out["us_per_step"] = {"hip_dropin": pc_hip, "c_oracle_1thread": pc_c}
 print(json.dumps(out))

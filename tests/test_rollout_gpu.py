@@ -40,8 +40,11 @@ def _run(map_size, n_side, E, T, max_steps):
     return recs, rc
 
 
+@pytest.mark.parametrize("pipe", ["0", "1"])
 @pytest.mark.parametrize("map_size,n_side,E,T,max_steps", [(24, 18, 3, 45, 20), (64, 128, 2, 70, 400)])
-def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps):
+def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps, pipe, monkeypatch):
+    """pipe 0: the fused k_rollout; 1: k_rollout_obs beside k_rollout<.., kSplit> (two state copies)."""
+    monkeypatch.setenv("MFX_ROLLOUT_PIPE", pipe)
     recs, rc = _run(map_size, n_side, E, T, max_steps)
     left, right = bd.block_positions(map_size, n_side)
     VF, F = 13 * 13 * 7, 34
@@ -81,10 +84,12 @@ def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps):
         del env
 
 
-def test_rollout_processes_every_env_once():
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_rollout_processes_every_env_once(pipe, monkeypatch):
     """The persistent work queue (k_env_order + per-launch counters) hands every env to exactly one
     workgroup per launch: before the armies meet no agent dies, so each env's agent-step counter
     must read 256 * steps.  E is not a multiple of the order kernel's 1024-env rounds."""
+    monkeypatch.setenv("MFX_ROLLOUT_PIPE", pipe)
     import torch
     from mfrl_amd.battle import BattleBatch
     E, steps = 5003, 3
@@ -162,3 +167,54 @@ def test_rollout_large_env_matches_oracle(map_size, n_side, E, T, max_steps):
                 env.add_agents(h[0], method="custom", pos=left)
                 env.add_agents(h[1], method="custom", pos=right)
     assert kills > 0                              # the attack fixed point saw real kills
+
+
+def test_rollout_pipe_state_handoff(monkeypatch):
+    """The pipeline's two state copies trade places every launch: after an odd number of launches the
+    per-call API must see the same state as the fused kernel leaves, and rollout steps after per-call
+    calls (a re-plan) must continue identically."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, VF, F = 3, 13 * 13 * 7, 34
+    left, right = bd.block_positions(64, 128)
+    engs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("MFX_ROLLOUT_PIPE", pipe)
+        eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.3, seed=3, stagger=False)
+        engs.append(eng)
+
+    def snap(eng):
+        rc = eng.rowcap
+        out = []
+        for g in range(2):
+            v = torch.zeros(E * rc * VF, dtype=torch.float32, device="cuda")
+            f = torch.zeros(E * rc * F, dtype=torch.float32, device="cuda")
+            eng.observe(g, v, f, rc)
+            out += [v, f]
+        n = torch.empty(E * 2, dtype=torch.int32, device="cuda")
+        eng.rollout_copy("group_num", n)
+        eng.sync()
+        return [x.cpu().numpy() for x in out + [n]]
+
+    def rollout_out(eng):
+        rc = eng.rowcap
+        out = []
+        for g in range(2):
+            v = torch.empty(E * rc * VF, dtype=torch.float32, device="cuda")
+            eng.rollout_copy("view", v, group=g)
+            out.append(v)
+        a = torch.empty(E * 2 * rc, dtype=torch.int32, device="cuda")
+        eng.rollout_copy("actions", a)
+        eng.sync()
+        return [x.cpu().numpy() for x in out + [a]]
+
+    for eng in engs:
+        eng.rollout_step(37)                     # odd: the pipeline's live state is its second copy
+    a, b = snap(engs[0]), snap(engs[1])
+    for x, y in zip(a, b):
+        assert x.tobytes() == y.tobytes()
+    for eng in engs:
+        eng.rollout_step(4)
+    for x, y in zip(rollout_out(engs[0]), rollout_out(engs[1])):
+        assert x.tobytes() == y.tobytes()
