@@ -1128,10 +1128,139 @@ __device__ __forceinline__ uint32_t minstd_jump(uint32_t x0, uint32_t k) {   // 
 }
 
 
+// Value of lane q of a wave-uniform loop (v_readlane: q must be uniform; ignores EXEC).
+__device__ __forceinline__ int lane_i(int x, int q) { return __builtin_amdgcn_readlane(x, q); }
+__device__ __forceinline__ float lane_f(float x, int q) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), q));
+}
+
+// attack_parallel for one wave (n <= 64): the same passes, with every per-position array that a lane
+// scans (j_k, the hits, their damage) held one entry per lane and read with v_readlane in
+// wave-uniform loops instead of a dependent chain of LDS loads; the fixed point keeps one "kills its
+// target here" bit per position, so a pass that changes nothing is a ballot.
+__device__ void attack_wave(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* atk, int n,
+                            uint32_t& rng, const ParScratch& ps, int nid) {
+    const int t = TID, W = gp.W, H = gp.H;
+    // ---- shuffle: element t sits at j_t, then moves to every later k with j_k == its position
+    uint32_t ent = 0;
+    int jv = -1;
+    if (t < n) {
+        ent = atk[t];
+        const uint32_t x = minstd_jump(rng, (uint32_t)t + 1u);
+        jv = (int)(x % (uint32_t)(t + 1));
+        if (t == n - 1) ps.flag[0] = (int)x;
+    }
+    for (int id = t; id < nid; id += 64) ps.death[id] = kNoDeath;
+    int p = jv;
+    for (int k = 1; k < n; ++k) {
+        const int jk = lane_i(jv, k);
+        if (k > t && jk == p) p = k;
+    }
+    if (t < n) ps.ord[p] = ent;
+    wave_sync_lds();
+    if (n > 0) rng = (uint32_t)ps.flag[0];
+    // ---- per position: attacker, damage, target at phase start
+    int A = -1, T = -2;
+    float dmg = 0.0f;
+    if (t < n) {
+        const uint32_t e2 = ps.ord[t];
+        A = (int)(e2 >> 8);
+        const int ai = (int)(e2 & 0xFF);
+        const uint32_t m = v.meta[A];
+        if (!meta_dead(m)) {
+            const int g = meta_group(m);
+            const SerialType& S = sm.tt[g];
+            const uint32_t pos = v.xy[A];
+            const int ox = (int)(pos & 0xFFFF) + S.att_x_off + S.att_dx[ai];
+            const int oy = (int)(pos >> 16) + S.att_y_off + S.att_dy[ai];
+            uint32_t cv = kCellEmpty;
+            if (ox >= 0 && ox < W && oy >= 0 && oy < H) cv = v.cells[oy * W + ox];
+            T = -1;
+            if (cv < kCellFood && (S.attack_in_group || (int)meta_group(v.meta[cv]) != g)) T = (int)cv;
+            dmg = S.damage;
+        }
+    }
+    const float hT = T >= 0 ? v.hp[T] : 0.0f;
+    wave_sync_lds();
+    // ---- fixed point on the death positions: kill = "this position's hit kills its target"
+    bool kill = false;
+    int eff = -1;
+    for (int it = 0; it <= n + 1; ++it) {
+        eff = (T >= 0 && ps.death[A] > t) ? T : -1;
+        bool nk = false;
+        if (eff >= 0) {
+            float h = hT;
+            bool stop = false;
+            for (int q = 0; q < n; ++q) {
+                const int eq = lane_i(eff, q);
+                const float dq = lane_f(dmg, q);
+                if (!stop && q <= t && eq == T) {
+                    h = h - dq;                                  // Agent::be_attack
+                    if (h < 0.0f) { stop = true; nk = q == t; }
+                }
+            }
+        }
+        if (__ballot(nk != kill) == 0ull) break;
+        wave_sync_lds();                                         // every death[A] read is done
+        if (kill && !nk) ps.death[T] = kNoDeath;
+        wave_sync_lds();
+        if (nk) ps.death[T] = (int16_t)t;
+        kill = nk;
+        wave_sync_lds();
+    }
+    // ---- apply: attackers (each agent attacks at most once per step), then hp, then deaths
+    eff = (T >= 0 && ps.death[A] > t && ps.death[T] >= t) ? T : -1;
+    bool last = false;
+    float hl = 0.0f;
+    if (eff >= 0) {                          // the last hit on T sets its hp: replay the hits up to it
+        last = true;
+        float h = hT;
+        for (int q = 0; q < n; ++q) {
+            const int eq = lane_i(eff, q);
+            const float dq = lane_f(dmg, q);
+            if (eq == T) {
+                if (q <= t) h = h - dq;
+                else last = false;
+            }
+        }
+        hl = h;
+    }
+    if (t < n && T != -2 && ps.death[A] > t) {
+        const uint32_t m = v.meta[A];
+        const int g = meta_group(m);
+        const SerialType& S = sm.tt[g];
+        if (eff < 0) {
+            v.next_r[A] += S.attack_penalty;                     // blank area (or a dead target)
+        } else {
+            const bool k = ps.death[T] == t;
+            v.meta[A] = (uint8_t)meta_make(0, k ? kOpKill : kOpAttack, g);
+            v.op_obj[A] = T;
+            const float reward = k ? sm.tt[meta_group(v.meta[T])].kill_reward : 0.0f;
+            v.next_r[A] += reward + S.attack_penalty;
+        }
+    }
+    wave_sync_lds();
+    if (last) v.hp[T] = hl;
+    for (int id = t; id < nid; id += 64) {
+        if (ps.death[id] == kNoDeath) continue;
+        const uint32_t om = v.meta[id];
+        const int og = meta_group(om);
+        v.meta[id] = (uint8_t)meta_make(1, meta_op(om), og);
+        v.next_r[id] = sm.tt[og].dead_penalty;
+        const uint32_t pos = v.xy[id];
+        v.cells[(pos >> 16) * W + (pos & 0xFFFF)] = kCellEmpty;   // remove_agent
+        atomicAdd(&v.grp_dead[og], 1);
+    }
+    wave_sync_lds();
+}
+
 // Shuffle + attack resolution for n_atk <= lanes.  Leaves the attack effects applied to v.
 template <bool kWave>
 __device__ void attack_parallel(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* atk,
                                 int n, uint32_t& rng, const ParScratch& ps, int nid) {
+#ifndef MFX_ATTACK_LDS_SCAN
+    if (kWave) { attack_wave(gp, sm, v, atk, n, rng, ps, nid); return; }
+#endif
     const int t = TID, W = gp.W, H = gp.H;
     // ---- shuffle
     uint32_t ent = 0;
