@@ -1368,10 +1368,60 @@ __device__ void attack_parallel(const GameParams& gp, const StepSmem& sm, EnvVie
     psync<kWave>();
 }
 
+// move_parallel for one wave (n <= 64).  A mover resolves once no earlier pending mover touches
+// its source or target cell; the cells never change, so each lane's set of earlier movers sharing a
+// cell is one 64-bit mask built once (v_readlane over the movers), and every round is a ballot.
+__device__ void move_wave(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n) {
+    const int t = TID, W = gp.W, H = gp.H;
+    int id = -1, src = -1, dst = -2, nx = 0, ny = 0;
+    bool pending = false;
+    if (t < n) {
+        const uint32_t ent = order[t];
+        id = (int)(ent >> 16);
+        const int mi = (int)((ent >> 8) & 0xFF);
+        const uint32_t m = v.meta[id];
+        if (!meta_dead(m)) {
+            const SerialType& S = sm.tt[meta_group(m)];
+            const uint32_t p = v.xy[id];
+            const int x = p & 0xFFFF, y = p >> 16;
+            nx = x + S.move_dx[mi]; ny = y + S.move_dy[mi];
+            // out of board: no-op; a move onto itself succeeds without changing anything
+            pending = !(nx < 0 || ny < 0 || nx + 1 >= W || ny + 1 >= H) && !(nx == x && ny == y);
+            src = y * W + x; dst = ny * W + nx;
+        }
+    }
+    if (!pending) { src = -1; dst = -2; }   // claims nothing
+    unsigned long long conf = 0;
+    for (int q = 0; q < n; ++q) {
+        const int sq = lane_i(src, q), dq = lane_i(dst, q);
+        if (q < t && (sq == src || sq == dst || dq == src || dq == dst)) conf |= 1ull << q;
+    }
+    unsigned long long pend = __ballot(pending);
+    while (pend) {
+        if (pending && (conf & pend) == 0) {
+            const uint32_t cv = v.cells[dst];
+            if (cv == kCellEmpty) {
+                v.cells[src] = kCellEmpty;
+                v.cells[dst] = (uint16_t)id;
+                v.xy[id] = (uint32_t)nx | ((uint32_t)ny << 16);
+            } else if (cv < kCellFood) {
+                v.meta[id] = (uint8_t)meta_make(0, kOpCollide, meta_group(v.meta[id]));
+                v.op_obj[id] = (int)cv;
+            }
+            pending = false;
+        }
+        wave_sync_lds();
+        pend = __ballot(pending);
+    }
+}
+
 // Move resolution for n_mov <= lanes in `order` (buffer order, or band order on large maps).
 template <bool kWave>
 __device__ void move_parallel(const GameParams& gp, const StepSmem& sm, EnvView& v, const uint32_t* order, int n,
                               const ParScratch& ps) {
+#ifndef MFX_MOVE_OWNER_ROUNDS
+    if (kWave) { move_wave(gp, sm, v, order, n); return; }
+#endif
     const int t = TID, W = gp.W, H = gp.H;
     int id = -1, src = 0, dst = 0, nx = 0, ny = 0;
     bool pending = false;
