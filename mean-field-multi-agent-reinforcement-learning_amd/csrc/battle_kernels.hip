@@ -341,6 +341,29 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
     __syncthreads();
 }
 
+// obs_minimap split for k_rollout, whose install already walks every listed agent: the histogram
+// and info words of agent id of group j (Battle shape) ...
+#ifndef MFX_MM_IN_INSTALL
+#define MFX_MM_IN_INSTALL 1
+#endif
+__device__ __forceinline__ void obs_minimap_add(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int j,
+                                                int id, uint32_t p) {
+    constexpr int VW = BattleShape::VW, VH = BattleShape::VH, NV = VW * VH;
+    const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
+    atomicAdd(&sm.hist[j * NV + ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw], 1);
+    sm.info[id] = __float_as_uint(v.hp[id] / gp.type[j].hp) | ((uint32_t)j << 31);
+}
+// ... and the conversion to densities once the histogram is complete (after a barrier)
+template <bool kB>
+__device__ __forceinline__ void obs_minimap_finish(const GameParams& gp, const EnvView& v, const ObsSmem& sm) {
+    constexpr int NV = BattleShape::VW * BattleShape::VH;
+    for (int i = TID; i < BattleShape::G * NV; i += blockDim.x) {   // in place: mm aliases hist
+        const int n = v.grp_n[i / NV];
+        sm.mm[i] = n ? (float)sm.hist[i] / (float)n : __uint_as_float(0xFFC00000u);
+    }
+    __syncthreads();
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));   // nontemporal-storable float4
 
 // Fill the staging rows of agents [a0, a0+k) of group g, then stream them to out_view.
@@ -3107,6 +3130,11 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         if (kPf) pf_install(pf, smem, sc, nrows);
         else install_sync(s, pt, e, G, v, sc);
         if (TID == 0) { misc[0] = 0; misc[1] = 0; misc[5] = o; }
+        constexpr bool kMmFused = kB && !kSplit && MFX_MM_IN_INSTALL;
+        if (kMmFused) {                          // the minimap histogram rides on the placement pass
+            obs_prologue(gp, osm, 0);
+            for (int i = TID; i < G * BattleShape::VW * BattleShape::VH; i += blockDim.x) osm.hist[i] = 0;
+        }
         __syncthreads();
         // the agents onto the walls-only cells: every listed agent is alive at an install (the lists
         // were compacted at the end of the env's previous step)
@@ -3116,6 +3144,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
                 const int id = v.grp_ids[q * cap + i];
                 const uint32_t p = v.xy[id];
                 if (!meta_dead(v.meta[id])) v.cells[(p >> 16) * gp.W + (p & 0xFFFF)] = (uint16_t)id;
+                if (kMmFused) obs_minimap_add(gp, v, osm, q, id, p);
             }
         }
         __syncthreads();
@@ -3129,8 +3158,12 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
         MFX_STAMP(1);
         // ---------------- get_observation for every group (k_rollout_obs in the pipeline)
         if (!kSplit) {
-            obs_prologue(gp, osm, 0);
-            obs_minimap<kB>(gp, v, osm, 0);          // one view size for every group (rollout_plan)
+            if (kB && MFX_MM_IN_INSTALL) {
+                obs_minimap_finish<kB>(gp, v, osm);
+            } else {
+                obs_prologue(gp, osm, 0);
+                obs_minimap<kB>(gp, v, osm, 0);      // one view size for every group (rollout_plan)
+            }
             MFX_STAMP(2);
             rollout_observe_groups<kB>(gp, ra, v, osm, e);
         }
