@@ -1555,7 +1555,8 @@ __host__ __device__ inline size_t big_region_bytes(int acap, int cap, bool full)
     const size_t j = move_jump_bytes(acap, cap);
     if (j > r) r = j;
     if (full) {
-        if ((size_t)cap * 5 > r) r = (size_t)cap * 5;          // k_rollout_big's staged xy + meta
+        // k_rollout_big's staged xy + meta + group lists
+        if ((size_t)cap * (5 + 2 * kMaxGroups) > r) r = (size_t)cap * (5 + 2 * kMaxGroups);
         if ((size_t)kBigOwnerSlots * 4 > r) r = (size_t)kBigOwnerSlots * 4;
         if ((size_t)17 * 1024 * 4 > r) r = (size_t)17 * 1024 * 4;     // band_sort_big: 16 bands x 1024 lanes
     }
@@ -3589,13 +3590,19 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
     // ---------------- policy + mean action (former_act_prob)
     // meta and positions of every id staged in LDS (the step scratch is free until the attacks): the
     // policy's and set_action's dependent lookups become LDS reads; the cells stay in HBM
-    EnvView vp = v;                        // (big_region_bytes holds cap * 5 bytes)
+    EnvView vp = v;                        // (big_region_bytes holds cap * (5 + 2 * kMaxGroups) bytes)
     {
         const int idc = s.id_counter[e];
         uint32_t* xy_l = reinterpret_cast<uint32_t*>(bs.base);
         uint8_t* meta_l = reinterpret_cast<uint8_t*>(bs.base + (size_t)cap * 4);
         for (int i = TID; i < idc; i += blockDim.x) { xy_l[i] = v.xy[i]; meta_l[i] = v.meta[i]; }
         vp.xy = xy_l; vp.meta = meta_l;
+#ifndef MFX_BIG_NO_IDS_STAGE
+        uint16_t* ids_l = reinterpret_cast<uint16_t*>(bs.base + (size_t)cap * 5);
+        for (int g = 0; g < G; ++g)
+            for (int i = TID; i < v.grp_n[g]; i += blockDim.x) ids_l[g * cap + i] = v.grp_ids[g * cap + i];
+        vp.grp_ids = ids_l;
+#endif
     }
     for (int i = TID; i < G * 64; i += blockDim.x) ahist[i] = 0;
     __syncthreads();
@@ -3610,7 +3617,7 @@ __global__ void __launch_bounds__(kBigRolloutThreads) k_rollout_big(const GamePa
             a[j] = -1; gg[j] = 0; ii[j] = i;
             if (i >= ntot) continue;
             while (i >= v.grp_n[g]) { i -= v.grp_n[g]; ++g; }
-            const int id = v.grp_ids[g * cap + i];
+            const int id = vp.grp_ids[g * cap + i];
             const uint32_t key = ekey ^ mix32((uint32_t)id * 0x85EBCA77u + (uint32_t)g);
             a[j] = rush_action(gp, sm.tt[g], vp, g, id, key, ra.eps);
             gg[j] = g; ii[j] = i;
