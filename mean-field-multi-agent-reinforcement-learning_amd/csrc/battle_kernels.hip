@@ -619,10 +619,10 @@ __device__ __forceinline__ CellObs obs_cell_post(const CellPre& p, uint32_t cv, 
 
 typedef __attribute__((address_space(1))) const uint16_t g_u16;
 
-// obs_stream_battle with the cells in HBM (large envs): each wave issues the cell loads of kObsPf (6:
-// +1.5-2.7 % at 256x256 over 4, 8 loses; profiles/r01_big_sweeps.txt)
+// obs_stream_battle with the cells in HBM (large envs): each wave issues the cell loads of kObsPf
 // 64-cell blocks back to back, then stages and flushes them one by one, so one HBM round trip is
-// paid per kObsPf blocks instead of per block.  The explicit global address space keeps the
+// paid per kObsPf blocks instead of per block (6: +1.5-2.7 % at 256x256 over 4; 8 loses;
+// profiles/r01_big_sweeps.txt).  The explicit global address space keeps the
 // loads off lgkmcnt (a flat load would be waited for by every LDS sync of the stream).
 #ifndef MFX_OBS_PF
 #define MFX_OBS_PF 6
