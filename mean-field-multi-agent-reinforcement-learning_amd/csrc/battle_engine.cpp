@@ -1035,7 +1035,8 @@ public:
                     ra.obs_items = ro_items.p; ra.obs_cnt = ro_cnt.p;
                     ra.obs_par_stride = (size_t)E * n_groups() * slots; ra.obs_item_rows = R;
                     MFX_HIP_THROW(observe_items_grid(gp, R, &ro_item_grid));
-                    ro_item_grid = std::max(1, ro_item_grid / kItemGridDiv);
+                    const char* gd = getenv("MFX_ITEM_GRID_DIV");   // sweeps only
+                    ro_item_grid = std::max(1, ro_item_grid / (gd ? std::max(1, atoi(gd)) : kItemGridDiv));
                 }
                 const int K = std::min(ro_split, E);
                 ro_sub_ctx.ensure(K);
