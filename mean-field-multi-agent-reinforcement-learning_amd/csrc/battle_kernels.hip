@@ -2621,7 +2621,8 @@ __host__ __device__ inline RolloutUnion rollout_union(const GameParams& gp, int 
 
 __host__ __device__ inline size_t rollout_scratch_bytes(const GameParams& gp, int cap, int acap, int rows, int threads,
                                                         bool kB) {
-    const size_t obs = obs_smem_core(gp, 0, cap, rows, obs_stage_floats(gp, 0, kB, threads), kB);
+    // (Battle shape: the agent records of every group at once, rollout_observe_groups)
+    const size_t obs = obs_smem_core(gp, 0, cap, rows * (kB ? gp.n_groups : 1), obs_stage_floats(gp, 0, kB, threads), kB);
     const size_t stp = rollout_union(gp, cap, acap, threads).total;
     return obs > stp ? obs : stp;
 }
@@ -3018,24 +3019,34 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
 template <bool kB>
 __device__ __forceinline__ void rollout_observe_groups(const GameParams& gp, const RolloutArgs& ra, const EnvView& v,
                                                        const ObsSmem& osm, int e) {
+    if (kB) {                                  // every group's records, one barrier, every group's stream
+        for (int g = 0; g < BattleShape::G; ++g) {
+            ObsSmem og = osm;
+            og.aq = osm.aq + g * ra.rowcap;
+            obs_agent_records(gp, v, og, g, min(v.grp_n[g], ra.rowcap));
+        }
+        __syncthreads();
+#ifndef MFX_DIAG_NO_OBS                              // diagnostic builds only: everything but the stream
+        for (int g = 0; g < BattleShape::G; ++g) {
+            constexpr size_t VF = (size_t)BattleShape::VW * BattleShape::VH * BattleShape::NC;
+            ObsSmem og = osm;
+            og.aq = osm.aq + g * ra.rowcap;
+            obs_stream_battle(gp, v, og, g, min(v.grp_n[g], ra.rowcap), ra.view[g] + (size_t)e * ra.rowcap * VF,
+                              ra.feat[g] + (size_t)e * ra.rowcap * BattleShape::F, osm.stage);
+        }
+#endif
+        __syncthreads();
+        return;
+    }
     for (int g = 0; g < gp.n_groups; ++g) {
         const TypeParams& T = gp.type[g];
         const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch;
         float* ov = ra.view[g] + (size_t)e * ra.rowcap * VF;
         float* of = ra.feat[g] + (size_t)e * ra.rowcap * gp.feat_size[g];
         const int n = min(v.grp_n[g], ra.rowcap);
-        if (kB) {
-            obs_agent_records(gp, v, osm, g, n);
-            __syncthreads();
-#ifndef MFX_DIAG_NO_OBS                              // diagnostic builds only: everything but the stream
-            obs_stream_battle(gp, v, osm, g, n, ov, of, osm.stage);
-#endif
-            __syncthreads();                   // the records are rebuilt for the next group
-        } else {
-            obs_prologue(gp, osm, g);
-            __syncthreads();
-            for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
-        }
+        obs_prologue(gp, osm, g);
+        __syncthreads();
+        for (int a0 = 0; a0 < n; a0 += kObsK) obs_rows<kB>(gp, v, osm, g, a0, min(kObsK, n - a0), ov, of);
     }
 }
 
@@ -3114,7 +3125,8 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
     const size_t soff = env_image_bytes(s.cells_n, cap, G);
     char* uni = smem + soff;                 // scratch shared by the observation and the step phases
     size_t soff2 = soff;
-    ObsSmem osm = carve_obs(smem, gp, 0, cap, ra.rowcap, obs_stage_floats(gp, 0, kB, blockDim.x), kB, soff2);
+    ObsSmem osm = carve_obs(smem, gp, 0, cap, ra.rowcap * (kB ? G : 1), obs_stage_floats(gp, 0, kB, blockDim.x), kB,
+                            soff2);
     if (!kB) osm.info = nullptr;
     const RolloutUnion u = rollout_union(gp, cap, acap, blockDim.x);
     int32_t* act = reinterpret_cast<int32_t*>(uni + u.act);
@@ -3320,7 +3332,8 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_OBS_OCC) k_rollout_ob
         EnvView v = carve_env(smem, s.cells_n, cap, G);
         v.grp_n = sc.grp_n; v.grp_dead = sc.grp_dead; v.grp_reward = sc.grp_reward;
         size_t soff = env_image_bytes(s.cells_n, cap, G);
-        ObsSmem osm = carve_obs(smem, gp, 0, cap, ra.rowcap, obs_stage_floats(gp, 0, kB, blockDim.x), kB, soff);
+        ObsSmem osm = carve_obs(smem, gp, 0, cap, ra.rowcap * (kB ? G : 1), obs_stage_floats(gp, 0, kB, blockDim.x),
+                                kB, soff);
         if (!kB) osm.info = nullptr;
         const int c4 = cap >> 2, sh = __ffs(c4) - 1;
         const int nc16 = s.cells_n >> 3, nrows = nc16 + image_small_rows(c4, G);
@@ -3883,7 +3896,7 @@ hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const St
 size_t rollout_obs_smem_bytes(const GameParams& gp, int cells_n, int cap, int rows) {
     const bool kB = is_battle_shape(gp);
     return env_image_bytes(cells_n, cap, gp.n_groups) +
-           obs_smem_core(gp, 0, cap, rows, obs_stage_floats(gp, 0, kB, MFX_ROLLOUT_THREADS), kB);
+           obs_smem_core(gp, 0, cap, rows * (kB ? gp.n_groups : 1), obs_stage_floats(gp, 0, kB, MFX_ROLLOUT_THREADS), kB);
 }
 
 hipError_t launch_rollout_obs(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
