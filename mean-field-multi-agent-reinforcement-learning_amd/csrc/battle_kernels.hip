@@ -3184,7 +3184,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
             MFX_STAMP(2);
             rollout_observe_groups<kB>(gp, ra, v, osm, e);
         }
-        __syncthreads();                       // the scratch region changes hands
+        if (kSplit) __syncthreads();           // (rollout_observe_groups ends with one: the scratch changes hands)
         MFX_STAMP(3);
         // ---------------- policy, set_action, step, get_reward, clear_dead (agent_phase)
         uint32_t rng = sc.rng;
@@ -3203,10 +3203,9 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
 #else
             if (ntot <= 64) {
 #endif
-                if (TID < 64)
+                if (TID < 64)                  // wave 0 (and its lane 0 below) alone; the others wait at
                     agent_phase<kB, true>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, &bs, e,
-                                          step_index, stamp_row, rng, done, kills);
-                __syncthreads();
+                                          step_index, stamp_row, rng, done, kills);   // the episode-end barrier
             } else {
 #ifndef MFX_DIAG_OBS_ONLY
                 agent_phase<kB, false>(gp, s, ra, v, sc, misc, sm, act, ahist, atk, mov, sorted, red, ps, &bs, e,
