@@ -346,12 +346,19 @@ __device__ __forceinline__ void obs_minimap(const GameParams& gp, const EnvView&
 #ifndef MFX_MM_IN_INSTALL
 #define MFX_MM_IN_INSTALL 1
 #endif
+// (and its agent record, obs_agent_records, when i < rows: list position i of group j)
 __device__ __forceinline__ void obs_minimap_add(const GameParams& gp, const EnvView& v, const ObsSmem& sm, int j,
-                                                int id, uint32_t p) {
+                                                int id, uint32_t p, int i, int rows) {
     constexpr int VW = BattleShape::VW, VH = BattleShape::VH, NV = VW * VH;
     const int sw = (gp.W + VW - 1) / VW, sh = (gp.H + VH - 1) / VH;
-    atomicAdd(&sm.hist[j * NV + ((int)(p >> 16) / sh) * VW + (int)(p & 0xFFFF) / sw], 1);
+    const int x = (int)(p & 0xFFFF), y = (int)(p >> 16);
+    const int b = (y / sh) * VW + x / sw;
+    atomicAdd(&sm.hist[j * NV + b], 1);
     sm.info[id] = __float_as_uint(v.hp[id] / gp.type[j].hp) | ((uint32_t)j << 31);
+    if (i < rows) {
+        const TypeParams& T = gp.type[j];
+        sm.aq[j * rows + i] = (uint32_t)(x + T.view_x1 + 8) | ((uint32_t)(y + T.view_y1 + 8) << 12) | ((uint32_t)b << 24);
+    }
 }
 // ... and the conversion to densities once the histogram is complete (after a barrier)
 template <bool kB>
@@ -3016,16 +3023,20 @@ __device__ __forceinline__ void agent_phase(const GameParams& gp, const State& s
 
 // get_observation of every group of the env in LDS (after obs_prologue + obs_minimap): rows of
 // env e in ra.view / ra.feat.
+// records_ready: the agent records were written with the minimap (obs_minimap_add) and a barrier
+// has passed since.
 template <bool kB>
 __device__ __forceinline__ void rollout_observe_groups(const GameParams& gp, const RolloutArgs& ra, const EnvView& v,
-                                                       const ObsSmem& osm, int e) {
+                                                       const ObsSmem& osm, int e, bool records_ready) {
     if (kB) {                                  // every group's records, one barrier, every group's stream
-        for (int g = 0; g < BattleShape::G; ++g) {
-            ObsSmem og = osm;
-            og.aq = osm.aq + g * ra.rowcap;
-            obs_agent_records(gp, v, og, g, min(v.grp_n[g], ra.rowcap));
+        if (!records_ready) {
+            for (int g = 0; g < BattleShape::G; ++g) {
+                ObsSmem og = osm;
+                og.aq = osm.aq + g * ra.rowcap;
+                obs_agent_records(gp, v, og, g, min(v.grp_n[g], ra.rowcap));
+            }
+            __syncthreads();
         }
-        __syncthreads();
 #ifndef MFX_DIAG_NO_OBS                              // diagnostic builds only: everything but the stream
         for (int g = 0; g < BattleShape::G; ++g) {
             constexpr size_t VF = (size_t)BattleShape::VW * BattleShape::VH * BattleShape::NC;
@@ -3161,7 +3172,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
                 const int id = v.grp_ids[q * cap + i];
                 const uint32_t p = v.xy[id];
                 if (!meta_dead(v.meta[id])) v.cells[(p >> 16) * gp.W + (p & 0xFFFF)] = (uint16_t)id;
-                if (kMmFused) obs_minimap_add(gp, v, osm, q, id, p);
+                if (kMmFused) obs_minimap_add(gp, v, osm, q, id, p, i, ra.rowcap);
             }
         }
         __syncthreads();
@@ -3182,7 +3193,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_ROLLOUT_OCC) k_rollou
                 obs_minimap<kB>(gp, v, osm, 0);      // one view size for every group (rollout_plan)
             }
             MFX_STAMP(2);
-            rollout_observe_groups<kB>(gp, ra, v, osm, e);
+            rollout_observe_groups<kB>(gp, ra, v, osm, e, kB && MFX_MM_IN_INSTALL);
         }
         if (kSplit) __syncthreads();           // (rollout_observe_groups ends with one: the scratch changes hands)
         MFX_STAMP(3);
@@ -3352,7 +3363,7 @@ __global__ void __launch_bounds__(MFX_ROLLOUT_THREADS, MFX_OBS_OCC) k_rollout_ob
         if (kPf && en < s.E) pf_issue(pf, pt, s, en, nrows, nc16, sh, c4);
         obs_prologue(gp, osm, 0);
         obs_minimap<kB>(gp, v, osm, 0);
-        rollout_observe_groups<kB>(gp, ra, v, osm, e);
+        rollout_observe_groups<kB>(gp, ra, v, osm, e, false);
         __syncthreads();                        // the image and the hand-off change hands
         e = en;
         en = misc[0];
