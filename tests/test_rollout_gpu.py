@@ -12,14 +12,14 @@ import common
 pytestmark = pytest.mark.gpu
 
 
-def _run(map_size, n_side, E, T, max_steps):
+def _run(map_size, n_side, E, T, max_steps, config="battle", VF=13 * 13 * 7, F=34):
     import torch
     from mfrl_amd.battle import BattleBatch
     left, right = bd.block_positions(map_size, n_side)
-    eng = BattleBatch(map_size, E, stream=torch.cuda.current_stream())
+    eng = BattleBatch(map_size, E, config=config, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=99, stagger=False)
     rc = eng.rowcap
-    VF, F = 13 * 13 * 7, 34
+    NA = eng.env.get_action_space(eng.handles[0])[0]
     recs = []
     for t in range(T):
         eng.rollout_step(1)
@@ -31,7 +31,7 @@ def _run(map_size, n_side, E, T, max_steps):
             eng.rollout_copy("feature", r["feat%d" % g], group=g)
         r["act"] = torch.empty(E * 2 * rc, dtype=torch.int32)
         r["rew"] = torch.empty(E * 2 * rc, dtype=torch.float32)
-        r["mean"] = torch.empty(E * 2 * 21, dtype=torch.float64)
+        r["mean"] = torch.empty(E * 2 * NA, dtype=torch.float64)
         eng.rollout_copy("actions", r["act"])
         eng.rollout_copy("rewards", r["rew"])
         eng.rollout_copy("mean_action", r["mean"])
@@ -218,3 +218,67 @@ def test_rollout_pipe_state_handoff(monkeypatch):
         eng.rollout_step(4)
     for x, y in zip(rollout_out(engs[0]), rollout_out(engs[1])):
         assert x.tobytes() == y.tobytes()
+
+
+def _generic_config(map_size):
+    """Battle rules with an 11x11 view, no minimap and 8-bit ids: not the Battle shape, so k_rollout runs
+    its generic observation path (obs_rows) and per-id minimap bins."""
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": map_size, "map_height": map_size, "minimap_mode": False, "embedding_size": 8})
+    attrs = dict(width=1, length=1, hp=10, speed=2, damage=2, step_recover=0.1, step_reward=-0.005,
+                 kill_reward=5, dead_penalty=-0.1, attack_penalty=-0.1,
+                 view_range=gw.CircleRange(5), attack_range=gw.CircleRange(1.5))
+    small = cfg.register_agent_type("small", attrs)
+    armies = [cfg.add_group(small), cfg.add_group(small)]
+    a, b = (gw.AgentSymbol(g, index="any") for g in armies)
+    cfg.add_reward_rule(gw.Event(a, "attack", b), receiver=a, value=0.2)
+    cfg.add_reward_rule(gw.Event(b, "attack", a), receiver=b, value=0.2)
+    return cfg
+
+
+def test_rollout_generic_shape_matches_oracle():
+    """k_rollout<kB = false> (a view size other than Battle's 13x13 and no minimap) against the oracle."""
+    import magent
+    map_size, n_side, E, T, max_steps = 32, 40, 2, 40, 30
+    cfg = _generic_config(map_size)
+    probe = common.config_env(common.ORACLE_LIB, cfg, map_size)[0]
+    ph = probe.get_handles()
+    vh, vw, nc = probe.get_view_space(ph[0])
+    F = probe.get_feature_space(ph[0])[0]
+    NA = probe.get_action_space(ph[0])[0]
+    VF = vh * vw * nc
+    assert (vh, vw) == (11, 11) and F != 34
+    del probe
+    recs, rc = _run(map_size, n_side, E, T, max_steps, config=cfg, VF=VF, F=F)
+    left, right = bd.block_positions(map_size, n_side)
+    for e in range(E):
+        env, h = common.config_env(common.ORACLE_LIB, cfg, map_size)
+        ep_len = 0
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        for t in range(T):
+            r = recs[t]
+            acts = []
+            for g in range(2):
+                v, f = env.get_observation(h[g])
+                n = len(v)
+                assert r["view%d" % g].reshape(E, rc, VF)[e, :n].tobytes() == v.reshape(n, VF).tobytes(), (e, t, g)
+                assert r["feat%d" % g].reshape(E, rc, F)[e, :n].tobytes() == f.tobytes(), (e, t, g)
+                acts.append(r["act"].reshape(E, 2, rc)[e, g, :n].astype(np.int32))
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rw = env.get_reward(h[g])
+                assert r["rew"].reshape(E, 2, rc)[e, g, :len(rw)].tobytes() == rw.tobytes(), (e, t, g, "reward")
+            env.clear_dead()
+            ep_len += 1
+            if done or ep_len >= max_steps:
+                ep_len = 0
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
+        del env
