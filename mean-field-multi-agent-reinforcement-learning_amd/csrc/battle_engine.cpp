@@ -140,6 +140,8 @@ public:
     uint64_t epoch = 1, n_ep = 0, obs_ep = 0, info_ep = 0;
     int hn[kMaxGroups] = {};                 // group sizes of env 0 (valid when n_ep == epoch)
     size_t obs_rows = 0, info_rows = 0;      // rows per group of the staging layouts below
+    bool obs_packed = false;                 // one env: pin_obs holds views|features per group packed
+    size_t obs_pack_off[kMaxGroups] = {};    //   at these float offsets
     DevBuf<uint8_t> st_info;                 // env 0's record (k_get_env0): header, then per group
                                              //   ids i32 | reward f32 | pos 2 x i32 | alive u8, x rows
     PinBuf<uint8_t> pin_obs, pin_info;       // host copies: views + features, info, in the same layouts
@@ -852,23 +854,40 @@ public:
         }
         try {
             obs_rows = std::max(obs_rows, (size_t)rowcap);
-            st_view.ensure((size_t)G * E * rowcap * vmax);
+            st_view.ensure((size_t)G * E * rowcap * (vmax + fmax));   // (+ fmax: the packed one-env layout)
             st_feat.ensure((size_t)G * E * rowcap * fmax);
             pin_obs.ensure((size_t)G * obs_rows * obs_row_bytes());
         } catch (const HipFailure& f) {
             return fail("%s", f.what());
         }
-        for (int g = 0; g < G; g++) {
-            if (!hn[g]) continue;
-            const TypeParams& T = gp.type[g];
-            const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
-            float* dv = st_view.p + (size_t)g * E * rowcap * vmax;
-            float* df = st_feat.p + (size_t)g * E * rowcap * fmax;
-            MFX_CHECK(observe(g, dv, df, rowcap));
-            uint8_t* hv = pin_obs.p + obs_off_view(g);
-            MFX_HIP(hipMemcpyAsync(hv, dv, sizeof(float) * hn[g] * VF, hipMemcpyDeviceToHost, stream));
-            MFX_HIP(hipMemcpyAsync(hv + sizeof(float) * obs_rows * VF, df, sizeof(float) * hn[g] * F,
-                                   hipMemcpyDeviceToHost, stream));
+        obs_packed = E == 1;
+        if (obs_packed) {
+            // one env: every group's views, each followed by its features, back to back in the
+            // staging buffer and in pin_obs -- one copy for all of it
+            size_t off = 0;
+            for (int g = 0; g < G; g++) {
+                const TypeParams& T = gp.type[g];
+                const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
+                obs_pack_off[g] = off;
+                if (!hn[g]) continue;
+                float* dv = st_view.p + off;
+                MFX_CHECK(observe(g, dv, dv + (size_t)hn[g] * VF, rowcap));
+                off += (size_t)hn[g] * (VF + F);
+            }
+            if (off) MFX_HIP(hipMemcpyAsync(pin_obs.p, st_view.p, sizeof(float) * off, hipMemcpyDeviceToHost, stream));
+        } else {
+            for (int g = 0; g < G; g++) {
+                if (!hn[g]) continue;
+                const TypeParams& T = gp.type[g];
+                const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
+                float* dv = st_view.p + (size_t)g * E * rowcap * vmax;
+                float* df = st_feat.p + (size_t)g * E * rowcap * fmax;
+                MFX_CHECK(observe(g, dv, df, rowcap));
+                uint8_t* hv = pin_obs.p + obs_off_view(g);
+                MFX_HIP(hipMemcpyAsync(hv, dv, sizeof(float) * hn[g] * VF, hipMemcpyDeviceToHost, stream));
+                MFX_HIP(hipMemcpyAsync(hv + sizeof(float) * obs_rows * VF, df, sizeof(float) * hn[g] * F,
+                                       hipMemcpyDeviceToHost, stream));
+            }
         }
         MFX_CHECK(queue_info());                 // this epoch's ids (and the error word) ride along
         MFX_HIP(hipStreamSynchronize(stream));
@@ -1192,6 +1211,12 @@ public:
         if (n == 0) return 0;
         const TypeParams& T = gp.type[g];
         const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
+        if (obs_packed) {
+            const float* hv = reinterpret_cast<const float*>(pin_obs.p) + obs_pack_off[g];
+            memcpy(bufs[0], hv, sizeof(float) * n * VF);
+            memcpy(bufs[1], hv + (size_t)n * VF, sizeof(float) * n * F);
+            return 0;
+        }
         const uint8_t* hv = pin_obs.p + obs_off_view(g);
         memcpy(bufs[0], hv, sizeof(float) * n * VF);
         memcpy(bufs[1], hv + sizeof(float) * obs_rows * VF, sizeof(float) * n * F);

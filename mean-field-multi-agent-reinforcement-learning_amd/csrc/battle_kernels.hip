@@ -232,7 +232,8 @@ hipError_t observe_items_grid(const GameParams& gp, int rows, int* grid) {
 
 hipError_t launch_observe(const GameParams& gp, const GameParams* d_gp, const State& s, int g, int max_n,
                           float* d_view, float* d_feat, int rowcap, hipStream_t st) {
-    const int chunk = 64;
+    // few envs (the drop-in's one env): 16-agent chunks, so one group's rows spread over more CUs
+    const int chunk = (long long)s.E * ((max_n + 63) / 64) < 256 ? 16 : 64;
     const int chunks = max(1, (max_n + chunk - 1) / chunk);
     const int cells_in_lds = (size_t)s.cells_n * 2 <= 32768;
     const size_t smem = observe_smem_bytes(gp, g, cells_in_lds, s.cells_n, s.cap);
