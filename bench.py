@@ -1,6 +1,6 @@
 """Throughput bench: Battle 64x64, 256 agents -- agent-steps/s of the hot path (env.step + obs).
 
-    python bench.py [--gpus N --steps K --warmup W] [--envs E] [--no-cpu-baseline]
+    python bench.py [--gpus N --steps K --warmup W] [--envs E | --total-envs T] [--no-cpu-baseline]
 
 Episodes are staggered over envs and the batch is run for one episode cap (400 steps) before
 the warmup, so any K-step window sees the steady mix of episode phases (not just the opening
@@ -8,14 +8,22 @@ the warmup, so any K-step window sees the steady mix of episode phases (not just
 every env of the batch: get_observation for both groups (views + features written to HBM),
 the synthetic rush policy of SURVEY.md 8(d) (on device), set_action, step (attack shuffle,
 attacks, starve, moves, reward rules, done), get_reward, mean-action pooling, clear_dead,
-and episode restart at done / 400 steps.  It is ONE kernel launch (k_rollout) per step.
+and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default 4) such
+steps of every env back to back while the env's image stays in LDS; the timed region is exactly K
+steps (K / substeps launches), bit-identical to K one-step launches.
 `value` counts agents present at get_observation, summed over envs, steps and ranks, over the
-max-over-ranks wall time of the K timed steps.  Multi-GPU: one process per GPU, each with its
-own E envs (weak scaling); the only collective is the RCCL all-reduce of episode statistics.
+max-over-ranks wall time of the K timed steps.
+
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is one
+rank; run directly with --gpus N > 1 it starts N fresh rank processes itself (before anything here
+touches the GPU) and exits with their status.  --envs E: E envs per rank (weak scaling);
+--total-envs T: T envs split over the ranks (strong scaling, configs[3]: 64 envs over 8 GPUs).
+The only collective is the RCCL all-reduce of the episode statistics.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -30,21 +38,33 @@ BYTES_PER_AGENT_STEP = 4 * (1183 + 34) + 4 + 4 + 1 + 4 + 64      # SURVEY.md 8(d
 HBM_PEAK_GBS = 8000.0                                           # MI355X spec (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 24576 at 64x64, 1024 at 256x256)")
+    ap.add_argument("--total-envs", type=int, default=None,
+                    help="envs over all GPUs, split evenly (strong scaling; configs[3]: --total-envs 64)")
     ap.add_argument("--map", type=int, default=MAP, help="map side (64: the metric's config; 256: configs[4])")
     ap.add_argument("--agents", type=int, default=2 * N_SIDE, help="agents per env, half per group")
     ap.add_argument("--max-steps", type=int, default=400)
+    # 4 consecutive steps of every env per k_rollout launch (env image kept in LDS between them): the
+    # launch ramp-up / tail and the env install / write-back are paid once per 4 steps, +9-11 % over one
+    # step per launch; 8 and 16 gain nothing more (profiles/r02_substeps_sweep.txt).  The results are
+    # bit-identical for any value (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps).
+    ap.add_argument("--substeps", type=int, default=4,
+                    help="consecutive steps of every env per k_rollout launch (env image kept in LDS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="concurrent single-thread CPU-baseline processes (default: the host cores this job may use)")
+    ap.add_argument("--cpu-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--backend", default="nccl", help=argparse.SUPPRESS)
-    a = ap.parse_args()
-    if a.envs is None:
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
+    a = ap.parse_args(argv)
+    if a.envs is None and a.total_envs is None:
         # 64x64: 24576 envs per GPU -- a launch has a fixed cost (~0.15 ms: ramp-up and the tail of the
         # persistent grid), amortised over more envs: 16384 -> 24576 envs = +6-11 % agent-steps/s,
         # beyond ~28K the gain stops (profiles/r01_env_sweep.txt)
@@ -52,8 +72,70 @@ def parse():
     return a
 
 
+def rank_envs(args, world, rank):
+    """Envs this rank steps: --envs per rank, or its share of --total-envs (remainder to low ranks)."""
+    if args.total_envs is None:
+        return args.envs
+    return args.total_envs // world + (1 if rank < args.total_envs % world else 0)
+
+
+# ----------------------------------------------------------------------------- N-rank launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (torch.distributed.run's env contract, 127.0.0.1
+    rendezvous) and wait for them.  Called before anything in this process touches the GPU; the
+    ranks are fresh children, so no GPU context is ever inherited or exec'd over.  If one rank
+    fails the others are stopped (they would wait at a barrier).  Returns the worst exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                status = status or rc
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
+def launcher_selftest(args):
+    """One rank of the launcher rehearsal (CPU, gloo): the same rank/env handling and reductions as the
+    GPU bench, without the engine.  Rank r 'processes' 100*(r+1) units in 0.01*(r+1) s."""
+    import torch
+    import torch.distributed as dist
+    from mfrl_amd.dist import reduce_stats, reduce_timing
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    E = rank_envs(args, world, rank)
+    red = reduce_stats(torch.ones(E, 4, dtype=torch.float64)).tolist()
+    elapsed, units = reduce_timing(0.01 * (rank + 1), 100 * (rank + 1), "cpu")
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "value": units / elapsed, "envs_total": red[0], "elapsed": elapsed}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(seconds, map_size=MAP, n_side=N_SIDE):
+def cpu_baseline(seconds, map_size=MAP, n_side=N_SIDE, seed=0):
     """Reference engine (oracle/_ref) if built, else the C oracle, single thread, same workload.
 
     Only env calls are timed (get_observation, get_agent_id, set_action, step, get_reward,
@@ -68,7 +150,7 @@ def cpu_baseline(seconds, map_size=MAP, n_side=N_SIDE):
     h = env.get_handles()
     _, v2a = env.get_view2attack(h[0])
     left, right = bd.block_positions(map_size, n_side)
-    rng = np.random.RandomState(0)
+    rng = np.random.RandomState(seed)
     clock, agent_steps, episodes = 0.0, 0, 0
     while clock < seconds:
         t = time.perf_counter()
@@ -96,29 +178,61 @@ def cpu_baseline(seconds, map_size=MAP, n_side=N_SIDE):
             agent_steps += len(obs[0][0]) + len(obs[1][0])
             k += 1
         episodes += 1
-    return {"value": agent_steps / clock, "unit": "agent-steps/s", "cores": 1, "kind": kind,
-            "sample": "%d agent-steps (%d episode starts) of Battle %dx%d/%d on 1 thread (OMP_NUM_THREADS=1), "
-                      "%.1f s of timed env calls; %s" % (agent_steps, episodes, map_size, map_size, 2 * n_side, clock,
-                                                         os.path.basename(path))}
+    return {"value": agent_steps / clock, "agent_steps": agent_steps, "episodes": episodes, "clock": clock,
+            "kind": kind, "lib": os.path.basename(path)}
 
 
-def run_cpu_baseline_subprocess(seconds, map_size, agents):
+def host_cores():
+    """(cores this job may use, cores the host shows).  On the GPU box `nproc` shows the whole
+    machine while one GPU's job gets a share of it (OMP_NUM_THREADS is set to that share there)."""
+    try:
+        shown = len(os.sched_getaffinity(0))
+    except AttributeError:
+        shown = os.cpu_count() or 1
+    share = os.environ.get("MFX_CPU_SHARE") or os.environ.get("OMP_NUM_THREADS")
+    use = min(shown, int(share)) if share and share.isdigit() and int(share) > 0 else shown
+    return max(1, use), shown
+
+
+def run_cpu_baseline(seconds, map_size, agents, procs=None):
+    """P concurrent single-thread reference-engine processes (OMP_NUM_THREADS=1: the reference attack
+    loop is racy with more threads, GridWorld.cc:522), one per host core of this job, each on its own
+    policy seed.  value = the sum of their rates (they run side by side for the same time)."""
+    use, shown = host_cores()
+    P = procs or use
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only",
-                          "--cpu-seconds", str(seconds), "--map", str(map_size), "--agents", str(agents)],
-                         env=env, capture_output=True, text=True, timeout=600)
-    if out.returncode != 0:
-        sys.stderr.write(out.stderr)
-        return None
-    return json.loads(out.stdout.strip().splitlines()[-1])
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--cpu-seconds", str(seconds),
+           "--map", str(map_size), "--agents", str(agents)]
+    ps = [subprocess.Popen(cmd + ["--cpu-seed", str(i)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True) for i in range(P)]
+    res = []
+    for p in ps:
+        out, err = p.communicate(timeout=600)
+        if p.returncode != 0:
+            sys.stderr.write(err)
+            return None
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    total = sum(r["value"] for r in res)
+    steps = sum(r["agent_steps"] for r in res)
+    return {"value": total, "unit": "agent-steps/s", "cores": P, "kind": res[0]["kind"],
+            "per_core": total / P, "host_nproc": shown,
+            "sample": "%d concurrent single-thread processes (OMP_NUM_THREADS=1), each %.0f s of timed env calls "
+                      "of Battle %dx%d/%d (rush policy outside the clock): %d agent-steps, %d episode starts in "
+                      "total; %s" % (P, seconds, map_size, map_size, agents, steps, sum(r["episodes"] for r in res),
+                                     res[0]["lib"])}
 
 
 # ----------------------------------------------------------------------------- GPU bench
 def main():
     args = parse()
     if args.cpu_baseline_only:
-        print(json.dumps(cpu_baseline(args.cpu_seconds, args.map, args.agents // 2)))
-        return
+        print(json.dumps(cpu_baseline(args.cpu_seconds, args.map, args.agents // 2, seed=args.cpu_seed)))
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if args.launcher_selftest:
+        launcher_selftest(args)
+        return 0
     import torch
     import torch.distributed as dist
     import battle_driver as bd
@@ -134,15 +248,16 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:                                # rehearsal of the N-rank flow without RCCL
             dist.init_process_group(args.backend)
+    E = rank_envs(args, world, rank)
     stream = torch.cuda.current_stream()
-
-    eng = BattleBatch(args.map, args.envs, stream=stream)
     left, right = bd.block_positions(args.map, args.agents // 2)
     from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing
+    eng = BattleBatch(args.map, E, stream=stream)
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
-    E = args.envs
+    S = max(1, args.substeps)
+    eng.rollout_substeps(S)
     grid, _ = eng.rollout_info()
-    big = grid == E and args.map * args.map > 64 * 64     # k_observe + k_rollout_big (state in HBM)
+    big = grid == E and args.map * args.map > 64 * 64     # k_observe_items + k_rollout_big (state in HBM)
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")
 
@@ -150,52 +265,62 @@ def main():
         eng.rollout_copy("agent_steps", steps_buf)
         return steps_buf.sum()
 
+    def stats():
+        eng.rollout_copy("stats", stats_buf)
+        return stats_buf.view(E, 4)
+
     # input preparation: run one episode cap of steps so that the staggered envs hold every
     # phase of an episode (early fights with ~256 agents ... late game with few survivors)
-    eng.rollout_step(args.max_steps)
-    for _ in range(args.warmup):
-        eng.rollout_step(1)
+    eng.rollout_step(args.max_steps + args.warmup)
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # launches of the timed region: S steps each (the last one the remainder); HIP events around each
+    # launch on the engine's stream
+    chunks = [min(S, args.steps - k) for k in range(0, args.steps, S)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in chunks]
     a0 = agent_steps()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     red = None
-    for k in range(args.steps):
+    done_steps = 0
+    for k, n in enumerate(chunks):
         ev[k][0].record(stream)
-        eng.rollout_step(1)
+        eng.rollout_step(n)
         ev[k][1].record(stream)
+        done_steps += n
         # episode statistics -> RCCL all-reduce, once per episode batch (an episode cap of steps) and at
         # the end of the timed window: the only collective
-        if world > 1 and ((k + 1) % args.max_steps == 0 or k == args.steps - 1):
-            eng.rollout_copy("stats", stats_buf)
-            red = reduce_stats(stats_buf.view(E, 4))
+        if world > 1 and (done_steps // args.max_steps != (done_steps - n) // args.max_steps or k == len(chunks) - 1):
+            red = reduce_stats(stats())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     a1 = agent_steps()
     if red is None:                  # one rank: the same statistics, reduced after the clock
-        eng.rollout_copy("stats", stats_buf)
-        red = reduce_stats(stats_buf.view(E, 4))
+        red = reduce_stats(stats())
     red = red.tolist()
-    kernel_ms = sum(s.elapsed_time(e) for s, e in ev) / args.steps
+    launch_ms = [s.elapsed_time(e) for s, e in ev]
+    # per-launch average over the full-size launches (a shorter remainder launch would skew it)
+    full = [t for t, n in zip(launch_ms, chunks) if n == S] or launch_ms
+    kernel_ms = sum(full) / len(full)
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
-        units_per_launch = local_units / args.steps
+        units_per_launch = local_units / args.steps * S
         achieved = BYTES_PER_AGENT_STEP * units_per_launch / (kernel_ms * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_big256.json" if big else "pmc_k_rollout.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("envs") == E and pm.get("map", MAP) == args.map:
+            if pm.get("envs") == E and pm.get("map", MAP) == args.map and pm.get("substeps", 1) == S:
                 traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_step"))
+        strong = args.total_envs is not None
+        kern = "k_observe_items+k_rollout_big" if big else "k_rollout"
         line = {
             "metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents" % (args.map, args.map, args.agents),
             "value": total_units / elapsed,
@@ -203,29 +328,35 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (fixed-seed two-block placement, on-device rush policy)",
-            "config": {"workload": "Battle %dx%d, %d+%d agents, %d envs per GPU, episode cap %d, %s"
-                       % (args.map, args.map, args.agents // 2, args.agents // 2, E, args.max_steps,
-                          "k_observe_items + k_rollout_big on 2 streams" if big else "fused step"),
-                       "map": args.map, "agents": args.agents, "envs_per_gpu": E,
+            "config": {"workload": "Battle %dx%d, %d+%d agents, %s, episode cap %d, %s"
+                       % (args.map, args.map, args.agents // 2, args.agents // 2,
+                          ("%d envs over %d GPUs" % (args.total_envs, world)) if strong else "%d envs per GPU" % E,
+                          args.max_steps,
+                          "k_observe_items + k_rollout_big on 2 streams" if big else
+                          ("fused step" if S == 1 else "fused step, %d consecutive steps per launch" % S)),
+                       "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S,
                        "parallelism": "envs sharded one process per GPU (dp%d)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_observe_items+k_rollout_big" if big else "k_rollout", "kernel_ms": kernel_ms,
+                         "kernel": kern, "kernel_ms": kernel_ms,
+                         "kernel_ms_is": "mean launch duration (HIP events on the launch stream), %d step(s) per launch"
+                                         % S if not big else "mean span of one step over its streams (HIP events)",
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch},
             "cpu_baseline": None,
             "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],
                          "kills": red[3], "note": "all ranks, since rollout_init (RCCL all-reduce per episode batch)"},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = run_cpu_baseline_subprocess(args.cpu_seconds, args.map, args.agents)
-        print(json.dumps(line))
+            line["cpu_baseline"] = run_cpu_baseline(args.cpu_seconds, args.map, args.agents, args.cpu_procs)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

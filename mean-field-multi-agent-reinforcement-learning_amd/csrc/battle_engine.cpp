@@ -174,6 +174,9 @@ public:
     DevBuf<RolloutCtx> ro_ctx;               // device copy of {s, ra} read by k_rollout
     RolloutCtx ro_ctx_host{};
     int ro_grid = 0, ro_cap = 0;
+    // fused rollout: consecutive steps of each env per k_rollout launch (env image kept in LDS between
+    // them; the launch's ramp-up / tail and the install / write-back are paid once per ro_sub steps)
+    int ro_sub = 1;
     // large-env path: the envs split into ro_split independent sub-batches, each a pipeline
     // (k_observe_items -> k_rollout_big) on its own stream, so one sub-batch's latency-bound step
     // overlaps the other's HBM-bound observation.  Each item launch takes a third of the chip's
@@ -1152,7 +1155,7 @@ public:
                 MFX_HIP(hipEventRecord(ro_ev[kMaxSplit], stream));
                 MFX_HIP(hipStreamWaitEvent(ro_str[0], ro_ev[kMaxSplit], 0));
                 MFX_HIP(launch_rollout_obs(gp, d_gp, s, c, ra.rowcap, ra.work_sel, qp, ro_obs_grid, ro_str[0]));
-                MFX_HIP(launch_rollout(gp, d_gp, s, c, ra.rowcap, ra.step_index, ra.work_sel, qp, ro_grid, 1, stream));
+                MFX_HIP(launch_rollout(gp, d_gp, s, c, ra.rowcap, ra.step_index, ra.work_sel, qp, ro_grid, 1, 1, stream));
                 MFX_HIP(hipEventRecord(ro_ev[0], ro_str[0]));
                 MFX_HIP(hipStreamWaitEvent(stream, ro_ev[0], 0));
                 swap_twin();                     // the written copy is the state now
@@ -1164,13 +1167,15 @@ public:
             }
             return 0;
         }
-        for (int i = 0; i < n_steps; i++) {
+        for (int i = 0; i < n_steps;) {
+            const int k = std::min(ro_sub, n_steps - i);
             MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
-                                   ro_grid, 0, stream));
+                                   ro_grid, 0, k, stream));
             ro_launch++;
-            ra.step_index++;
+            ra.step_index += k;
             ra.work_sel ^= 1;
-            cells_stale = n_steps > 0;
+            cells_stale = true;
+            i += k;
         }
         return 0;
     }
@@ -1657,6 +1662,17 @@ MFX_API int mfx_battle_rollout_copy(void* game, const char* name, int group, voi
     MFX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, e->stream));
     return 0;
 }
+// The same for bytes [offset, offset + bytes) of the buffer (e.g. one env's rows).
+MFX_API int mfx_battle_rollout_copy_at(void* game, const char* name, int group, size_t offset, void* dst, size_t bytes) {
+    BattleEngine* e = MFX_ENV(game);
+    void* src = nullptr;
+    size_t n = 0;
+    MFX_CHECK(e->rollout_buffer(name, group, &src, &n));
+    if (offset > n || bytes > n - offset)
+        return mfx::fail("rollout_copy_at: bytes [%zu, %zu) outside the buffer (%zu)", offset, offset + bytes, n);
+    MFX_HIP(hipMemcpyAsync(dst, static_cast<const char*>(src) + offset, bytes, hipMemcpyDefault, e->stream));
+    return 0;
+}
 // Diagnostic build only: route k_rollout phase stamps ([E][16] u64 s_memtime) to d_buf.
 MFX_API int mfx_battle_set_stamp_buffer(void* d_buf) {
     MFX_HIP(mfx::set_stamp_buffer((unsigned long long*)d_buf));
@@ -1665,6 +1681,15 @@ MFX_API int mfx_battle_set_stamp_buffer(void* d_buf) {
 // Launch geometry of the fused rollout: persistent grid (workgroups) and LDS bytes per workgroup.
 MFX_API int mfx_battle_rollout_info(void* game, int* grid, int* lds_bytes) {
     MFX_GUARD(MFX_ENV(game)->rollout_info(grid, lds_bytes));
+}
+
+// Steps per k_rollout launch (1..64): every env runs that many consecutive steps while its image stays
+// in LDS.  rollout_step(n) results are identical for any value (the last step's buffers, the same
+// state); only the launch count changes.  Ignored by the pipeline and the large-env path.
+MFX_API int mfx_battle_rollout_set_substeps(void* game, int n_sub) {
+    if (n_sub < 1 || n_sub > 64) return mfx::fail("rollout_set_substeps: %d not in 1..64", n_sub);
+    MFX_ENV(game)->ro_sub = n_sub;
+    return 0;
 }
 
 MFX_API int mfx_battle_rollout_rowcap(void* game, int* rowcap) {

@@ -318,11 +318,11 @@ static hipError_t with_rollout_obs_kernel(const GameParams& gp, const State& s, 
 
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                           int rows, uint32_t step_index, int work_sel, int qphase, int grid, int split,
-                          hipStream_t st) {
+                          int n_sub, hipStream_t st) {
     const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rows);
-    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    if (smem > 160 * 1024 || n_sub < 1 || (split && n_sub != 1)) return hipErrorInvalidValue;
     return with_rollout_kernel(gp, s, split != 0, [&](auto kern) {
-        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel, qphase);
+        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel, qphase, n_sub);
         return hipGetLastError();
     });
 }

@@ -31,7 +31,8 @@ class BattleBatch:
                    "mfx_battle_set_action", "mfx_battle_step", "mfx_battle_get", "mfx_battle_clear_dead",
                    "mfx_battle_sync", "mfx_battle_rollout_init", "mfx_battle_rollout_step",
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
-                   "mfx_battle_rollout_info", "mfx_battle_group_capacity"):
+                   "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
+                   "mfx_battle_rollout_copy_at"):
             getattr(self._dll, fn).restype = ctypes.c_int
         self._dll.mfx_last_error.restype = ctypes.c_char_p
         self.handles = self.env.get_handles()
@@ -111,6 +112,10 @@ class BattleBatch:
         self._check(self._dll.mfx_battle_rollout_info(self.game, ctypes.byref(g), ctypes.byref(b)), "rollout_info")
         return g.value, b.value
 
+    def rollout_substeps(self, n_sub):
+        """Consecutive steps of every env per k_rollout launch (results do not depend on it)."""
+        self._check(self._dll.mfx_battle_rollout_set_substeps(self.game, int(n_sub)), "rollout_set_substeps")
+
     def rollout_step(self, n_steps=1):
         self._check(self._dll.mfx_battle_rollout_step(self.game, n_steps), "rollout_step")
 
@@ -121,3 +126,12 @@ class BattleBatch:
                                                   else dst.nbytes)
         self._check(self._dll.mfx_battle_rollout_copy(self.game, name.encode(), group, ctypes.c_void_p(ptr),
                                                       ctypes.c_size_t(size)), "rollout_copy")
+
+    def rollout_copy_at(self, name, dst, offset, group=0, nbytes=None):
+        """Copy bytes [offset, offset + nbytes) of a device rollout buffer into dst."""
+        ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else dst.ctypes.data
+        size = nbytes if nbytes is not None else (dst.numel() * dst.element_size() if hasattr(dst, "numel")
+                                                  else dst.nbytes)
+        self._check(self._dll.mfx_battle_rollout_copy_at(self.game, name.encode(), group, ctypes.c_size_t(offset),
+                                                         ctypes.c_void_p(ptr), ctypes.c_size_t(size)),
+                    "rollout_copy_at")

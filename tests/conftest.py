@@ -13,6 +13,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "mean-field-multi-agent-reinforcement-learning_amd")
 sys.path.insert(0, os.path.join(PKG, "python"))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.append(REPO)
 
 
 def pytest_configure(config):

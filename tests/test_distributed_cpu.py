@@ -1,6 +1,7 @@
 """The N>1 bench plumbing on CPU: world_size 2 over gloo (the GPU box uses RCCL through the same
 calls).  Checks the max-over-ranks time, the summed agent-steps and the stats all-reduce."""
 import os
+import sys
 import socket
 
 import pytest
@@ -39,3 +40,49 @@ def test_two_rank_reductions():
         assert u == 300.0               # 100 + 200
         assert red == [9.0] * 4         # 3 envs x (1 + 2)
     assert out[0][3] != out[1][3]       # distinct per-rank streams
+
+
+def _bench(*args, timeout=300):
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + list(args), env=env,
+                         capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("world,total", [(2, 64), (3, 64)])
+def test_bench_launcher_spawns_ranks(world, total):
+    """bench.py --gpus N run directly starts N rank processes itself (the parent never touches the GPU):
+    rank 0 prints one line with n_gpus N, the units summed over ranks over the max rank time, and the
+    --total-envs split (configs[3]: 64 envs over the ranks) reduced over every rank."""
+    line = _bench("--gpus", str(world), "--total-envs", str(total), "--launcher-selftest", "--backend", "gloo")
+    assert line["n_gpus"] == world
+    assert line["envs_total"] == total
+    units = sum(100 * (r + 1) for r in range(world))
+    assert abs(line["value"] - units / (0.01 * world)) < 1e-6
+
+
+def test_bench_launcher_propagates_failure():
+    """A rank that fails makes the launcher fail (and stops the other ranks)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launcher-selftest",
+                          "--no-such-flag"], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0
+
+
+def test_cpu_baseline_uses_several_cores():
+    """The CPU baseline runs one single-thread reference process per host core it is given and
+    reports the aggregate with the core count."""
+    import bench
+    res = bench.run_cpu_baseline(1.0, 64, 256, procs=2)
+    assert res is not None and res["cores"] == 2
+    assert res["value"] > 0 and abs(res["per_core"] * 2 - res["value"]) < 1e-6
+    use, shown = bench.host_cores()
+    assert 1 <= use <= shown

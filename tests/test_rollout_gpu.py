@@ -86,9 +86,10 @@ def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps, pipe, monkeyp
 
 @pytest.mark.parametrize("pipe", ["0", "1"])
 def test_rollout_processes_every_env_once(pipe, monkeypatch):
-    """The persistent work queue (k_env_order + per-launch counters) hands every env to exactly one
-    workgroup per launch: before the armies meet no agent dies, so each env's agent-step counter
-    must read 256 * steps.  E is not a multiple of the order kernel's 1024-env rounds."""
+    """The persistent work queue (the heaviest-first class lists filed by the previous launch, read
+    through the per-launch counter) hands every env to exactly one workgroup per launch: before the
+    armies meet no agent dies, so each env's agent-step counter must read 256 * steps.  E (5003) is
+    not a multiple of the persistent grid or of the filing buffer (32 envs per flush)."""
     monkeypatch.setenv("MFX_ROLLOUT_PIPE", pipe)
     import torch
     from mfrl_amd.battle import BattleBatch
@@ -282,3 +283,134 @@ def test_rollout_generic_shape_matches_oracle():
                 env.add_agents(h[0], method="custom", pos=left)
                 env.add_agents(h[1], method="custom", pos=right)
         del env
+
+
+def _sample_envs(E, k=16):
+    """k envs spread over the batch, both ends included (env E-1 has the shortest first episode)."""
+    return sorted(set([0, 1, E // 2, E - 2, E - 1] + [int(x) for x in np.linspace(0, E - 1, k - 5)]))[:k]
+
+
+def test_rollout_bench_shape_matches_oracle():
+    """The bench's own batch shape: 4096 staggered envs (the persistent grid is smaller than E, so the
+    heaviest-first class queue, the register prefetch of the next env and the queue hand-off are all
+    live), 450 steps (every env restarts at least once).  16 sampled envs are replayed on the C oracle
+    step by step with the actions the device policy chose: views, features, rewards and the mean action
+    bit for bit.  Stagger: env e's first episode starts at length e * max_steps // E
+    (BattleEngine::rollout_init)."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, T, max_steps, VF, F = 4096, 450, 400, 13 * 13 * 7, 34
+    left, right = bd.block_positions(64, 128)
+    eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=1234, stagger=True)
+    grid, _ = eng.rollout_info()
+    assert grid < E                                  # the work queue hands out envs
+    rc = eng.rowcap
+    sample = _sample_envs(E)
+    envs = []
+    for e in sample:
+        env, h = common.battle_env(common.ORACLE_LIB, 64)
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        envs.append([env, h, e * max_steps // E])
+    view = torch.empty((len(sample), 2, rc, VF), dtype=torch.float32).pin_memory()
+    feat = torch.empty((len(sample), 2, rc, F), dtype=torch.float32).pin_memory()
+    act = torch.empty((len(sample), 2, rc), dtype=torch.int32).pin_memory()
+    rew = torch.empty((len(sample), 2, rc), dtype=torch.float32).pin_memory()
+    mean = torch.empty((len(sample), 2, 21), dtype=torch.float64).pin_memory()
+    restarts = 0
+    for t in range(T):
+        eng.rollout_step(1)
+        for j, e in enumerate(sample):
+            for g in range(2):
+                eng.rollout_copy_at("view", view[j, g], e * rc * VF * 4, group=g)
+                eng.rollout_copy_at("feature", feat[j, g], e * rc * F * 4, group=g)
+            eng.rollout_copy_at("actions", act[j], e * 2 * rc * 4)
+            eng.rollout_copy_at("rewards", rew[j], e * 2 * rc * 4)
+            eng.rollout_copy_at("mean_action", mean[j], e * 2 * 21 * 8)
+        eng.sync()
+        for j, st in enumerate(envs):
+            env, h, _ = st
+            acts = []
+            for g in range(2):
+                v, f = env.get_observation(h[g])
+                n = len(v)
+                assert view[j, g, :n].numpy().tobytes() == v.reshape(n, VF).tobytes(), (sample[j], t, g, "view")
+                assert feat[j, g, :n].numpy().tobytes() == f.tobytes(), (sample[j], t, g, "feature")
+                a = act[j, g, :n].numpy().astype(np.int32)
+                acts.append(a)
+                m = np.mean(list(map(lambda x: np.eye(21)[x], a)), axis=0) if n else np.full(21, np.nan)
+                assert np.array_equal(mean[j, g].numpy(), m, equal_nan=True), (sample[j], t, g, "mean")
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rw = env.get_reward(h[g])
+                assert rew[j, g, :len(rw)].numpy().tobytes() == rw.tobytes(), (sample[j], t, g, "reward")
+            env.clear_dead()
+            st[2] += 1
+            if done or st[2] >= max_steps:
+                st[2] = 0
+                restarts += 1
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
+    assert restarts >= len(sample)
+
+
+@pytest.mark.parametrize("sub", [2, 7])
+def test_rollout_substeps_match_single_steps(sub):
+    """k_rollout running `sub` consecutive steps of each env per launch (image kept in LDS) leaves
+    exactly what single-step launches leave: every output buffer, the episode statistics, the
+    agent-step counters and the state the per-call API observes, after a partial episode and again
+    after a full episode cap (restarts inside a launch).  Together with the oracle replay above this
+    pins the multi-step launch."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E = 3000
+    left, right = bd.block_positions(64, 128)
+    engs = []
+    for s in (1, sub):
+        eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=77, stagger=True)
+        eng.rollout_substeps(s)
+        engs.append(eng)
+
+    def dump(eng):
+        out = []
+        for name, dt in (("actions", torch.int32), ("rewards", torch.float32), ("mean_action", torch.float64),
+                         ("stats", torch.float64), ("agent_steps", torch.int64), ("group_num", torch.int32),
+                         ("episode_return", torch.float32)):
+            import ctypes
+            ptr, nb = ctypes.c_void_p(), ctypes.c_size_t()
+            eng._dll.mfx_battle_rollout_buffer(eng.game, name.encode(), 0, ctypes.byref(ptr), ctypes.byref(nb))
+            x = torch.empty(nb.value // torch.tensor([], dtype=dt).element_size(), dtype=dt, device="cuda")
+            eng.rollout_copy(name, x)
+            out.append(x)
+        for g in range(2):
+            for name, w in (("view", 13 * 13 * 7), ("feature", 34)):
+                x = torch.empty(E * eng.rowcap * w, dtype=torch.float32, device="cuda")
+                eng.rollout_copy(name, x, group=g)
+                out.append(x)
+        return out
+
+    for n in (37, 400):
+        for eng in engs:
+            eng.rollout_step(n)
+        a, b = dump(engs[0]), dump(engs[1])
+        torch.cuda.synchronize()
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x.view(torch.uint8) if x.dtype != torch.uint8 else x,
+                               y.view(torch.uint8) if y.dtype != torch.uint8 else y), (n, k)
+        del a, b
+    # and the per-call API sees the same state (cells rebuilt from the fused rollout's image)
+    rc = engs[0].rowcap
+    snaps = []
+    for eng in engs:
+        v = torch.zeros(E * rc * 13 * 13 * 7, dtype=torch.float32, device="cuda")
+        f = torch.zeros(E * rc * 34, dtype=torch.float32, device="cuda")
+        eng.observe(1, v, f, rc)
+        eng.sync()
+        snaps.append((v, f))
+    assert torch.equal(snaps[0][0], snaps[1][0]) and torch.equal(snaps[0][1], snaps[1][1])
