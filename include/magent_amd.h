@@ -128,9 +128,10 @@ int mfx_mean_action(const int32_t *d_acts, const int32_t *d_counts, int B, int r
 /* algo/base.py:192-220 */
 int mfx_mfq_target(const float *d_eq, const float *d_tq, const float *d_r, const uint8_t *d_done, int M, int A,
                    double gamma, double *d_out, void *stream);
-/* algo/ac.py:305-320 */
-int mfx_mfac_returns(float *d_rew, const int64_t *d_offsets, const float *d_value, int n_ep, float gamma,
-                     void *stream);
+/* algo/ac.py:305-320 -- numpy1 = 1: the reference's NumPy-1 promotion (float64 running return, the
+ * default of the python wrapper); 0: NEP-50 (float32), as the same lines run under NumPy 2 */
+int mfx_mfac_returns(float *d_rew, const int64_t *d_offsets, const float *d_value, int n_ep, double gamma,
+                     int numpy1, void *stream);
 
 /* ---------------------------------------------------------------- library */
 const char *mfx_last_error(void);

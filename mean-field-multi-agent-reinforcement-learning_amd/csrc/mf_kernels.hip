@@ -52,16 +52,31 @@ __global__ void __launch_bounds__(256) k_mfq_target(const float* __restrict__ e_
 }
 
 // One lane per episode: rewards[offsets[e] .. offsets[e+1]) are replaced by their discounted
-// returns, bootstrapped from value[e] (float32 throughout, numpy's float32 * python-float rule).
+// returns, bootstrapped from value[e] (algo/ac.py:312-320: keep = keep * gamma + r[i]; r[i] = keep).
+// numpy1 = 1: the reference's NumPy-1 promotion (its TF1 era) -- np.float32 * python float is float64,
+// so keep runs in float64 from the first step on and each r[i] is keep rounded to float32.
+// numpy1 = 0: NEP 50 (NumPy 2) -- keep stays float32 and gamma is rounded to float32 first.
+// Both pinned by tests/golden/algo_mfac_returns.npz (the reference's own loop, make_algo_fixtures.py).
 __global__ void __launch_bounds__(256) k_mfac_returns(float* __restrict__ rew, const int64_t* __restrict__ offsets,
-                                                      const float* __restrict__ value, int n_ep, float gamma) {
+                                                      const float* __restrict__ value, int n_ep, double gamma,
+                                                      int numpy1) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n_ep) return;
-    float keep = value[e];
-    for (int64_t i = offsets[e + 1] - 1; i >= offsets[e]; --i) {
-        const float t = keep * gamma;
-        keep = t + rew[i];
-        rew[i] = keep;
+    if (numpy1) {
+        double keep = (double)value[e];
+        for (int64_t i = offsets[e + 1] - 1; i >= offsets[e]; --i) {
+            const double t = keep * gamma;
+            keep = t + (double)rew[i];
+            rew[i] = (float)keep;
+        }
+    } else {
+        const float g = (float)gamma;
+        float keep = value[e];
+        for (int64_t i = offsets[e + 1] - 1; i >= offsets[e]; --i) {
+            const float t = keep * g;
+            keep = t + rew[i];
+            rew[i] = keep;
+        }
     }
 }
 
@@ -90,10 +105,12 @@ MFX_API int mfx_mfq_target(const float* d_eq, const float* d_tq, const float* d_
 }
 
 // rewards (in place) [offsets[n_ep]] f32, offsets [n_ep + 1] i64, value [n_ep] f32
-MFX_API int mfx_mfac_returns(float* d_rew, const int64_t* d_offsets, const float* d_value, int n_ep, float gamma,
-                             void* stream) {
+MFX_API int mfx_mfac_returns(float* d_rew, const int64_t* d_offsets, const float* d_value, int n_ep, double gamma,
+                             int numpy1, void* stream) {
+    if (n_ep < 0) return mfx::fail("mfac_returns: n_ep must be >= 0");
     if (n_ep == 0) return 0;
-    mfx::k_mfac_returns<<<(n_ep + 255) / 256, 256, 0, (hipStream_t)stream>>>(d_rew, d_offsets, d_value, n_ep, gamma);
+    mfx::k_mfac_returns<<<(n_ep + 255) / 256, 256, 0, (hipStream_t)stream>>>(d_rew, d_offsets, d_value, n_ep, gamma,
+                                                                             numpy1 != 0);
     MFX_HIP(hipGetLastError());
     return 0;
 }

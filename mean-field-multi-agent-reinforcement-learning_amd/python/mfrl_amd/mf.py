@@ -2,7 +2,8 @@
 
     mean_action(actions, counts, n_action)   senario_battle.py:141 (former_act_prob), float64
     mfq_target(e_q, t_q, rewards, dones, g)  algo/base.py:192-220 (ValueNet.calc_target_q), float64
-    mfac_returns(rewards, offsets, values, g) algo/ac.py:305-320 (discounted returns), float32
+    mfac_returns(rewards, offsets, values, g) algo/ac.py:305-320 (discounted returns, float64 running
+                                             return stored as float32: the reference's NumPy-1 rules)
 """
 import ctypes
 
@@ -42,10 +43,12 @@ def mfq_target(e_q, t_q, rewards, dones, gamma=0.95):
     return out
 
 
-def mfac_returns(rewards, offsets, values, gamma=0.95):
-    """Per-episode discounted returns, in place on float32 rewards; offsets int64 [E+1]."""
+def mfac_returns(rewards, offsets, values, gamma=0.95, numpy1=True):
+    """Per-episode discounted returns, in place on float32 rewards; offsets int64 [E+1].
+
+    numpy1: the promotion of the reference's NumPy-1 era (keep in float64); False: NEP 50 (float32)."""
     L = lib()
     L.mfx_mfac_returns.restype = ctypes.c_int
     check(L.mfx_mfac_returns(_p(rewards), _p(offsets.contiguous()), _p(values.contiguous()), len(values),
-                             ctypes.c_float(gamma), _stream()), "mfx_mfac_returns")
+                             ctypes.c_double(gamma), int(bool(numpy1)), _stream()), "mfx_mfac_returns")
     return rewards

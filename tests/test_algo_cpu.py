@@ -1,7 +1,8 @@
-"""mfrl_amd.algo on the CPU: the device replay buffers (run with device='cpu') against the numpy
-restatement of the reference's buffers (oracle/algo_oracle.py) under the same np.random stream;
-network shapes; the epsilon schedule.  PARITY UNPINNED against the reference itself: its algo
-package imports TensorFlow, which this image lacks."""
+"""mfrl_amd.algo on the CPU: the device replay buffers (run with device='cpu') against the outputs of
+the reference's own MemoryGroup / EpisodesBuffer (tests/golden/algo_replay.npz, recorded by
+make_algo_fixtures.py under a tensorflow stub) and against the numpy restatement
+oracle/algo_oracle.py, under the same np.random stream; network shapes; the epsilon schedule.  The
+networks themselves stay PARITY UNPINNED (their numerics need TensorFlow)."""
 import os
 import sys
 
@@ -110,3 +111,51 @@ def test_linear_decay_schedule():
     assert abs(linear_decay(800, x, y) - 0.6) < 1e-12
     assert abs(linear_decay(1600, x, y) - 0.2) < 1e-12
     assert abs(linear_decay(2000, x, y) - 0.1) < 1e-12
+
+
+def _reference_replay_check(device):
+    """The device replay buffers against the reference's own MemoryGroup / EpisodesBuffer outputs
+    (tests/golden/algo_replay.npz, recorded by make_algo_fixtures.py from algo/tools.py:26-362):
+    every sample() batch bit for bit under the same seeded np.random stream, get_batch_num, and the
+    EpisodesBuffer per-agent order, rewards, views and probs."""
+    sys.path.insert(0, common.GOLDEN)
+    import make_algo_fixtures as mk
+    fx = np.load(os.path.join(common.GOLDEN, "algo_replay.npz"))
+    V, F, A = mk.REPLAY_V, mk.REPLAY_F, mk.REPLAY_A
+    for ci, (use_mean, sub_len, max_len) in enumerate(mk.REPLAY_CASES):
+        key = "c%d_" % ci
+        mg = tools.MemoryGroup(V, F, A, max_len, 64, sub_len, use_mean=use_mean, device=device)
+        pushes = mk.replay_pushes(ci)
+        k = 0
+        for ep in range(3):
+            for e, p in pushes:
+                if e == ep:
+                    mg.push(state=[p["obs"], p["feat"]], acts=p["acts"], rewards=p["rewards"], alives=p["alives"],
+                            ids=p["ids"], prob=p["prob"])
+            np.random.seed(100 + ep)
+            mg.tight()
+            assert mg.get_batch_num() == fx[key + "nbatch"][ep], (ci, ep)
+            for b in range(2):
+                np.random.seed(1000 * ep + b)
+                got = mg.sample()
+                for j, g in enumerate(got):
+                    want = fx[key + "s%d_%d" % (k, j)]
+                    g = g.cpu().numpy()
+                    assert g.dtype == want.dtype and g.shape == want.shape, (ci, k, j)
+                    assert g.tobytes() == want.tobytes(), (ci, ep, b, j)
+                k += 1
+        assert k == int(fx[key + "nsample"])
+    eb = tools.EpisodesBuffer(use_mean=True, device=device)
+    np.random.seed(9)
+    for p in mk.episodes_pushes():
+        eb.push(state=[p["obs"], p["feat"]], acts=p["acts"], rewards=p["rewards"], alives=p["alives"], ids=p["ids"],
+                prob=p["prob"])
+    rows, counts = eb.batch()
+    assert counts.cpu().numpy().tolist() == fx["eb_counts"].tolist()
+    assert rows["rew"].cpu().numpy().tobytes() == fx["eb_rewards"].tobytes()
+    assert rows["obs"].cpu().numpy().tobytes() == fx["eb_obs"].astype(np.float32).tobytes()
+    assert rows["prob"].cpu().numpy().tobytes() == fx["eb_probs"].astype(np.float32).tobytes()
+
+
+def test_replay_matches_reference_fixture():
+    _reference_replay_check("cpu")

@@ -1,7 +1,8 @@
 """mfrl_amd.algo on the GPU: the MF-Q target through the HIP kernel
 against a torch float64 restatement of algo/base.py:192-220, act / train / soft update on device,
 one self-play round on the single-env drop-in and on the batched engine (observations never leave
-HBM).  The networks' numerics are PARITY UNPINNED (TensorFlow absent)."""
+HBM); the HBM replay rings against the reference's own MemoryGroup outputs.  The networks' numerics
+are PARITY UNPINNED (TensorFlow absent)."""
 import numpy as np
 import pytest
 import torch
@@ -119,3 +120,10 @@ def test_graph_train_matches_eager(algo):
         twin.update()
     for a, b in zip(m.vars, twin.vars):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
+def test_device_replay_matches_reference_fixture():
+    """The HBM replay rings (device='cuda') against the reference's own MemoryGroup / EpisodesBuffer
+    outputs (tests/golden/algo_replay.npz), bit for bit."""
+    import test_algo_cpu
+    test_algo_cpu._reference_replay_check("cuda")

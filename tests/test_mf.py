@@ -1,8 +1,10 @@
 """Mean-field kernels: mean-action pooling, MF-Q target, MF-AC returns.
 
-CPU part: the oracle's mean action equals what the reference loop recorded in the Battle fixtures.
-GPU part: the HIP kernels equal the oracle bit for bit (float64 / float32 as the reference's numpy
-dtype rules dictate).  MF-Q target and MF-AC returns are parity-unpinned (TensorFlow absent)."""
+CPU part: the oracle's mean action equals what the reference loop recorded in the Battle fixtures;
+the oracle's MF-Q target and MF-AC returns equal the outputs of the reference's own algo/ lines
+(tests/golden/algo_*.npz, run under a tensorflow stub by tests/golden/make_algo_fixtures.py).
+GPU part: the HIP kernels equal those fixtures and the oracle bit for bit (float64 / float32 as the
+reference's numpy dtype rules dictate)."""
 import os
 import sys
 
@@ -22,6 +24,33 @@ def test_oracle_mean_action_matches_fixture():
     for t in range(0, len(n), 37):
         for g in range(2):
             assert mf_oracle.mean_action(acts[t][g], 21)[0].tobytes() == fx["e0_mean_action"][t, g].tobytes()
+
+
+def _fx(name):
+    return np.load(os.path.join(common.GOLDEN, name))
+
+
+def test_oracle_mfq_target_matches_reference():
+    fx = _fx("algo_mfq_target.npz")
+    for b in range(int(fx["n_batches"])):
+        got = mf_oracle.mfq_target(fx["b%d_eq" % b], fx["b%d_tq" % b], fx["b%d_r" % b], fx["b%d_done" % b])
+        assert got.tobytes() == fx["b%d_target" % b].tobytes(), b
+
+
+def _episodes(fx):
+    offs = np.concatenate([[0], np.cumsum(fx["lens"])]).astype(np.int64)
+    return offs, [fx["rewards"][offs[e]:offs[e + 1]] for e in range(len(fx["lens"]))]
+
+
+@pytest.mark.parametrize("numpy1", [True, False])
+def test_oracle_mfac_returns_matches_reference(numpy1):
+    """Both promotion rules against the reference's MFAC.train loop; they differ in most entries."""
+    fx = _fx("algo_mfac_returns.npz")
+    offs, eps = _episodes(fx)
+    got = np.concatenate([mf_oracle.mfac_returns(r, v, numpy1=numpy1) for r, v in zip(eps, fx["value"])])
+    want = fx["returns_numpy1" if numpy1 else "returns_nep50"]
+    assert got.tobytes() == want.tobytes()
+    assert (fx["returns_numpy1"] != fx["returns_nep50"]).sum() > len(want) // 2
 
 
 def test_oracle_target_dtype_is_float64():
@@ -66,7 +95,33 @@ def test_mfq_target_kernel():
 
 
 @pytest.mark.gpu
-def test_mfac_returns_kernel():
+def test_mfq_target_kernel_matches_reference_vectors():
+    import torch
+    from mfrl_amd.mf import mfq_target
+    fx = _fx("algo_mfq_target.npz")
+    for b in range(int(fx["n_batches"])):
+        args = [torch.tensor(fx["b%d_%s" % (b, k)], device="cuda") for k in ("eq", "tq", "r")]
+        d = torch.tensor(fx["b%d_done" % b].astype(np.uint8), device="cuda")
+        got = mfq_target(*args, d).cpu().numpy()
+        assert got.tobytes() == fx["b%d_target" % b].tobytes(), b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numpy1", [True, False])
+def test_mfac_returns_kernel_matches_reference_vectors(numpy1):
+    import torch
+    from mfrl_amd.mf import mfac_returns
+    fx = _fx("algo_mfac_returns.npz")
+    offs, _ = _episodes(fx)
+    t = torch.tensor(fx["rewards"], device="cuda")
+    mfac_returns(t, torch.tensor(offs, device="cuda"), torch.tensor(fx["value"], device="cuda"), 0.95, numpy1=numpy1)
+    want = fx["returns_numpy1" if numpy1 else "returns_nep50"]
+    assert t.cpu().numpy().tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numpy1", [True, False])
+def test_mfac_returns_kernel(numpy1):
     import torch
     from mfrl_amd.mf import mfac_returns
     rs = np.random.RandomState(3)
@@ -75,7 +130,7 @@ def test_mfac_returns_kernel():
     rew = rs.randn(offs[-1]).astype(np.float32)
     val = rs.randn(50).astype(np.float32)
     t = torch.tensor(rew, device="cuda")
-    mfac_returns(t, torch.tensor(offs, device="cuda"), torch.tensor(val, device="cuda"))
+    mfac_returns(t, torch.tensor(offs, device="cuda"), torch.tensor(val, device="cuda"), numpy1=numpy1)
     got = t.cpu().numpy()
-    ref = np.concatenate([mf_oracle.mfac_returns(rew[offs[e]:offs[e + 1]], val[e]) for e in range(50)])
+    ref = np.concatenate([mf_oracle.mfac_returns(rew[offs[e]:offs[e + 1]], val[e], numpy1=numpy1) for e in range(50)])
     assert got.tobytes() == ref.tobytes()
