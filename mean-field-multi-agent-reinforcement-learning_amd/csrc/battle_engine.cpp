@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -129,6 +130,7 @@ public:
     int max_ids = 0;                                 // upper bound of id_counter over envs
     std::vector<int> group_ub;                       // upper bound of grp_n per group
     int pending_ub = 0;                              // upper bound of queued actions
+    int acts_since_step[kMaxGroups] = {};            // set_action calls per group since the last step
     // drop-in staging (env 0, host buffers)
     DevBuf<float> st_view, st_feat, st_f32;
     // Drop-in host cache (env 0).  The reference call sequence asks the same state many times per step
@@ -147,6 +149,28 @@ public:
     PinBuf<uint8_t> pin_obs, pin_info;       // host copies: views + features, info, in the same layouts
     PinBuf<int32_t> pin_act;                 // [G][rows] actions on their way to the device
     hipEvent_t act_ev[kMaxGroups] = {};      // that copy of group g has left pin_act
+    const uint8_t* info_src = nullptr;       // the record the getters answer from (pin_info or pin_fast)
+    size_t info_src_rows = 0;                //   and its rows per group
+    // Fast drop-in step (k_dropin_step, battle/dropin.inc): set_action and clear_dead are deferred and
+    // env.step() is ONE launch that also leaves the records of the post-step and post-clear_dead states
+    // and the next observation in host-mapped memory.  Deferred work runs for real (flush_deferred)
+    // before anything else reads or changes the device state.
+    bool fast_enabled = fast_default();      // MFX_DROPIN_FAST=0: the per-call path (A/B, tests)
+    static bool fast_default() {
+        const char* v = getenv("MFX_DROPIN_FAST");
+        return !v || atoi(v) != 0;
+    }
+    bool defer_act[kMaxGroups] = {};         // group g's actions wait in pin_fact
+    int defer_n[kMaxGroups] = {};
+    bool defer_clear = false;                // clear_dead waits for the next k_dropin_step
+    uint64_t spec_ep = 0;                    // epoch at which rec_clear / the observation blocks apply
+    bool obs_fast = false;                   // the observation cache is pin_fast's blocks
+    MappedBuf<uint8_t> pin_fast;             // rec_step | rec_clear | per group view block, feature block
+    MappedBuf<int32_t> pin_fact;             // [G][fact_rows] deferred actions
+    MappedBuf<uint32_t> pin_flag;            // [2] k_dropin_step's completion words (coherent)
+    uint32_t fast_seq = 0;                   // sequence number of the last k_dropin_step launch
+    size_t fast_rows = 0, fact_rows = 0;
+    size_t fast_rec_clear = 0, fast_view[kMaxGroups] = {}, fast_feat[kMaxGroups] = {};
     DevBuf<int> st_i32, st_xs, st_ys, st_dirs;
     DevBuf<uint8_t> st_u8;
     // fused rollout (bench / throughput path)
@@ -227,14 +251,12 @@ public:
         RolloutArgs q = ra;
         const int G = n_groups();
         const size_t rc = (size_t)ra.rowcap;
-        int na = 0;
         for (int g = 0; g < G; g++) {
             const TypeParams& T = gp.type[g];
             q.view[g] += e0 * rc * T.view_w * T.view_h * gp.n_ch;
             q.feat[g] += e0 * rc * gp.feat_size[g];
-            na = std::max(na, T.n_action);
         }
-        q.actions += e0 * G * rc; q.rewards += e0 * G * rc; q.mean_act += (size_t)e0 * G * na;
+        q.actions += e0 * G * rc; q.rewards += e0 * G * rc; q.mean_act += (size_t)e0 * G * ra.mean_stride;
         q.ep_return += (size_t)e0 * G; q.ep_len += e0; q.stats += (size_t)e0 * 4; q.agent_steps += e0;
         if (q.obs_mm) { q.obs_mm += (size_t)e0 * G * 169; q.obs_info += (size_t)e0 * s.cap; }
         q.env_base = e0;
@@ -656,7 +678,9 @@ public:
     }
 
     int reset() {
+        MFX_CHECK(flush_deferred());
         touch();
+        for (int g = 0; g < kMaxGroups; g++) acts_since_step[g] = 0;
         ro_prep_stale = true;
         MFX_CHECK(build_params());
         try {
@@ -699,6 +723,7 @@ public:
 
     // same placement for every env (host arrays)
     int add_agents(int group, int n, const char* method, const int* xs, const int* ys, const int* dirs) {
+        MFX_CHECK(flush_deferred());
         touch();
         ro_prep_stale = true;
         if (!allocated) return fail("add_agents before reset");
@@ -747,6 +772,7 @@ public:
 
     // GridWorld::set_goal (GridWorld.cc:729-740): "random" only, goals never read back.
     int set_goal(int group, const char* method) {
+        MFX_CHECK(flush_deferred());
         touch();
         if (strcmp(method, "random")) return fail("invalid goal type in GridWorld::set_goal");
         if (!allocated || group < 0 || group >= n_groups()) return fail("set_goal: bad state or group");
@@ -784,14 +810,15 @@ public:
     // ids | rewards | positions | alive, info_rows rows each
     static constexpr size_t kInfoRowBytes = 4 + 4 + 8 + 1;
     size_t info_region() const { return ((info_rows * kInfoRowBytes) + 15) & ~(size_t)15; }
-    size_t info_off(int g, int what) const {
-        const size_t base = 64 + (size_t)g * info_region();
+    size_t info_off(int g, int what) const {         // in the record at info_src
+        const size_t r = info_src_rows;
+        const size_t base = 64 + (size_t)g * (((r * kInfoRowBytes) + 15) & ~(size_t)15);
         if (what == kGetId) return base;
-        if (what == kGetReward) return base + info_rows * 4;
-        if (what == kGetPos) return base + info_rows * 8;
-        return base + info_rows * 16;                                // kGetAlive
+        if (what == kGetReward) return base + r * 4;
+        if (what == kGetPos) return base + r * 8;
+        return base + r * 16;                                        // kGetAlive
     }
-    const int32_t* info_hdr() const { return reinterpret_cast<const int32_t*>(pin_info.p); }
+    const int32_t* info_hdr() const { return reinterpret_cast<const int32_t*>(info_src); }
 
     // Queue the record's launch and its one copy to pinned memory (no sync).
     int queue_info() {
@@ -810,8 +837,11 @@ public:
         return 0;
     }
 
-    // after the sync that follows queue_info: this epoch's group sizes and info are on the host
-    int take_info() {
+    // after the sync that follows queue_info (or k_dropin_step): this epoch's group sizes and info are
+    // on the host, in the record at src
+    int take_info(const uint8_t* src = nullptr, size_t rows = 0) {
+        info_src = src ? src : pin_info.p;
+        info_src_rows = src ? rows : info_rows;
         for (int g = 0; g < n_groups(); g++) hn[g] = info_hdr()[g];
         n_ep = info_ep = epoch;
         return report_err(info_hdr()[kMaxGroups]);
@@ -819,6 +849,7 @@ public:
 
     int ensure_info() {
         if (info_ep == epoch) return 0;
+        MFX_CHECK(flush_deferred());
         MFX_CHECK(queue_info());
         MFX_HIP(hipStreamSynchronize(stream));
         return take_info();
@@ -844,7 +875,9 @@ public:
     // views + features of every group of env 0 (and the info of the same epoch) in one transfer
     int ensure_obs() {
         if (obs_ep == epoch) return 0;
+        MFX_CHECK(flush_deferred());
         MFX_CHECK(ensure_counts());
+        obs_fast = false;
         const int G = n_groups();
         int rowcap = 4;
         for (int g = 0; g < G; g++) rowcap = std::max(rowcap, group_ub[g]);
@@ -910,34 +943,48 @@ public:
 
     int observe(int g, float* d_view, float* d_feat, int rowcap) {
         if (!allocated || g < 0 || g >= n_groups()) return fail("observe: bad state or group");
+        MFX_CHECK(flush_deferred());
         MFX_CHECK(sync_cells());
         MFX_HIP(launch_observe(gp, d_gp, s, g, group_ub[g], d_view, d_feat, rowcap, stream));
         return 0;
     }
     int set_action(int g, const int* d_actions, int rowcap) {
+        MFX_CHECK(flush_deferred());
         touch();
+        if (g >= 0 && g < kMaxGroups) acts_since_step[g]++;
         if (!allocated || g < 0 || g >= n_groups()) return fail("set_action: bad state or group");
         pending_ub += group_ub[g];
         try { ensure_capacity(0, pending_ub); } catch (const HipFailure& f) { return fail("%s", f.what()); }
         MFX_HIP(launch_set_action(d_gp, s, g, d_actions, rowcap, stream));
         return 0;
     }
+    // A group's set_action called twice before a step: the serial forms (see State::serial_step).
+    void begin_step() {
+        s.serial_step = 0;
+        for (int g = 0; g < kMaxGroups; g++) { s.serial_step |= acts_since_step[g] > 1; acts_since_step[g] = 0; }
+    }
     int step(int* d_done) {
+        MFX_CHECK(flush_deferred());
         touch();
         ro_prep_stale = true;
         if (!allocated) return fail("step before reset");
         MFX_CHECK(sync_cells());
-        MFX_HIP(launch_step(gp, d_gp, s, max_ids, d_sort, stream));
+        begin_step();
+        const hipError_t le = launch_step(gp, d_gp, s, max_ids, d_sort, stream);
+        s.serial_step = 0;
+        MFX_HIP(le);
         pending_ub = 0;
         if (d_done) MFX_HIP(hipMemcpyAsync(d_done, s.done, sizeof(int32_t) * E, hipMemcpyDeviceToDevice, stream));
         return 0;
     }
     int get(int g, int what, void* d_out, int rowcap) {
         if (!allocated || g < 0 || g >= n_groups()) return fail("get: bad state or group");
+        MFX_CHECK(flush_deferred());
         MFX_HIP(launch_get(d_gp, s, g, what, d_out, rowcap, stream));
         return 0;
     }
     int clear_dead() {
+        MFX_CHECK(flush_deferred());
         touch();
         ro_prep_stale = true;
         if (!allocated) return fail("clear_dead before reset");
@@ -950,6 +997,7 @@ public:
     // followed by an immediate reset + placement of every env.
     int rollout_init(const int* tmpl_n, const int* const* xs, const int* const* ys, int max_steps, float eps,
                      uint32_t seed, int stagger) {
+        MFX_CHECK(flush_deferred());
         const int G = n_groups();
         if (!allocated) MFX_CHECK(reset());
         int total = 0, rowcap = 4, tcap = 1;
@@ -999,6 +1047,7 @@ public:
             MFX_HIP_THROW(hipMemset(ro_stats.p, 0, sizeof(double) * E * 4));
             MFX_HIP_THROW(hipMemset(ro_steps.p, 0, sizeof(unsigned long long) * E));
             a.rowcap = rowcap; a.actions = ro_actions.p; a.rewards = ro_rewards.p; a.mean_act = ro_mean.p;
+            a.mean_stride = na;
             a.ep_return = ro_return.p; a.ep_len = ro_eplen.p; a.stats = ro_stats.p; a.agent_steps = ro_steps.p;
             a.tmpl_x = ro_tx.p; a.tmpl_y = ro_ty.p; a.tmpl_cap = tcap;
             a.max_steps = max_steps; a.policy_seed = seed; a.step_index = 0; a.eps = eps;
@@ -1106,6 +1155,7 @@ public:
     }
 
     int rollout_step(int n_steps) {
+        MFX_CHECK(flush_deferred());
         touch();
         if (!rollout_ready) return fail("rollout_step before rollout_init");
         if (walls_after_init) return fail("rollout: walls added after rollout_init are not part of the rollout's episodes");
@@ -1208,6 +1258,162 @@ public:
     }
 
     // ------------------------------------------------------------------ drop-in (env 0, host buffers)
+    // The fast step applies to one env whose config the fused rollout supports and whose image plus
+    // step / observation scratch fits one workgroup's LDS.
+    size_t fast_rows_now() const {
+        size_t r = 4;
+        for (int g = 0; g < n_groups(); g++) r = std::max(r, (size_t)group_ub[g]);
+        return (r + 3) & ~(size_t)3;
+    }
+    bool fast_dropin_ok() const {
+        if (!fast_enabled || E != 1 || !allocated || gp.dsl || turn || food) return false;
+        for (int g = 0; g < n_groups(); g++) {
+            const TypeParams& T = gp.type[g];
+            if (T.body_w != 1 || T.body_h != 1 || T.view_w != gp.type[0].view_w || T.view_h != gp.type[0].view_h)
+                return false;
+        }
+        return dropin_smem_bytes(gp, s.cells_n, s.cap, s.acap, (int)fast_rows_now()) <= 160 * 1024;
+    }
+    // Run deferred set_action / clear_dead for real, in call order (clear_dead came first).
+    int flush_deferred() {
+        bool acts = false;
+        for (int g = 0; g < kMaxGroups; g++) acts |= defer_act[g];
+        spec_ep = 0;
+        if (!defer_clear && !acts) return 0;
+        if (defer_clear) {
+            defer_clear = false;
+            MFX_HIP(launch_clear_dead(d_gp, s, stream));
+        }
+        for (int g = 0; g < n_groups(); g++) {
+            if (!defer_act[g]) continue;
+            defer_act[g] = false;
+            const int rowcap = std::max(group_ub[g], 1);
+            try { st_i32.ensure((size_t)E * rowcap); } catch (const HipFailure& f) { return fail("%s", f.what()); }
+            if (defer_n[g])
+                MFX_HIP(hipMemcpyAsync(st_i32.p, pin_fact.p + (size_t)g * fact_rows, sizeof(int) * defer_n[g],
+                                       hipMemcpyHostToDevice, stream));
+            MFX_HIP(launch_set_action(d_gp, s, g, st_i32.p, rowcap, stream));
+        }
+        if (acts) MFX_HIP(hipStreamSynchronize(stream));   // pin_fact may be rewritten next
+        return 0;
+    }
+    // set_action deferred: the actions wait in host-mapped memory for the step's launch.
+    int fast_set_action(int g, const int* actions) {
+        if (defer_act[g]) MFX_CHECK(flush_deferred());      // a second call for the group before a step
+        const int n = num_env0(g);
+        const size_t rows = fast_rows_now();
+        try {
+            if (fact_rows < rows || pin_fact.n < (size_t)n_groups() * rows) {
+                MFX_CHECK(flush_deferred());
+                MFX_HIP_THROW(hipStreamSynchronize(stream));
+                fact_rows = std::max(fact_rows, rows);
+                pin_fact.ensure((size_t)n_groups() * fact_rows);
+            }
+            pending_ub += group_ub[g];
+            ensure_capacity(0, pending_ub);
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        if (n) memcpy(pin_fact.p + (size_t)g * fact_rows, actions, sizeof(int) * n);
+        acts_since_step[g]++;
+        defer_act[g] = true;
+        defer_n[g] = n;
+        const int keep_n = n_ep == epoch;
+        touch();
+        ro_prep_stale = true;
+        spec_ep = 0;
+        if (keep_n) n_ep = epoch;                           // group sizes do not change
+        return 0;
+    }
+    // env.step(): one k_dropin_step launch and one sync.
+    int fast_step(int* done) {
+        touch();
+        ro_prep_stale = true;
+        MFX_CHECK(sync_cells());
+        const int G = n_groups();
+        const size_t rows = fast_rows_now();
+        DropinArgs da{};
+        try {
+            const size_t rec = (64 + (size_t)G * (((rows * kInfoRowBytes) + 15) & ~(size_t)15) + 255) & ~(size_t)255;
+            const size_t rec_clear = rec;
+            size_t off = 2 * rec;
+            size_t vo[kMaxGroups], fo[kMaxGroups];
+            for (int g = 0; g < G; g++) {
+                const TypeParams& T = gp.type[g];
+                vo[g] = off; off = (off + rows * T.view_w * T.view_h * gp.n_ch * 4 + 255) & ~(size_t)255;
+                fo[g] = off; off = (off + rows * gp.feat_size[g] * 4 + 255) & ~(size_t)255;
+            }
+            if (pin_fast.n < off) {
+                MFX_HIP_THROW(hipStreamSynchronize(stream));   // the last launch may still write it
+                pin_fast.ensure(off);
+            }
+            if (!pin_flag.p) {
+                pin_flag.ensure(2, hipHostMallocCoherent);
+                pin_flag.p[0] = pin_flag.p[1] = 0;
+            }
+            fast_rows = rows;
+            fast_rec_clear = rec_clear;
+            for (int g = 0; g < G; g++) { fast_view[g] = vo[g]; fast_feat[g] = fo[g]; }
+        } catch (const HipFailure& f) {
+            return fail("%s", f.what());
+        }
+        for (int g = 0; g < G; g++) {
+            da.acts[g] = defer_act[g] ? pin_fact.d + (size_t)g * fact_rows : nullptr;
+            da.n_acts[g] = defer_act[g] ? defer_n[g] : 0;
+            da.view[g] = reinterpret_cast<float*>(pin_fast.d + fast_view[g]);
+            da.feat[g] = reinterpret_cast<float*>(pin_fast.d + fast_feat[g]);
+        }
+        da.pending_clear = defer_clear;
+        da.rows = (int)rows;
+        da.rec_step = pin_fast.d;
+        da.rec_clear = pin_fast.d + fast_rec_clear;
+        da.flag = pin_flag.d;
+        da.seq = ++fast_seq;
+        begin_step();
+        const hipError_t le = launch_dropin_step(gp, d_gp, s, da, stream);
+        s.serial_step = 0;
+        MFX_HIP(le);
+        MFX_CHECK(wait_fast(0));                  // the records; the observation is still being written
+        defer_clear = false;
+        for (int g = 0; g < kMaxGroups; g++) defer_act[g] = false;
+        pending_ub = 0;
+        MFX_CHECK(take_info(pin_fast.p, rows));
+        *done = info_hdr()[kMaxGroups + 1];
+        spec_ep = epoch;
+        return 0;
+    }
+    // Spin on k_dropin_step's completion word `which` (0 records, 1 observation) of launch fast_seq.
+    // The stream is polled now and then, so a failed or faulted launch is reported instead of awaited.
+    int wait_fast(int which) {
+        volatile uint32_t* f = pin_flag.p + which;
+        for (uint32_t k = 1;; k++) {
+            if (*f == fast_seq) break;
+            if ((k & 255) == 0) {
+                const hipError_t q = hipStreamQuery(stream);
+                if (q == hipSuccess) {
+                    if (*f == fast_seq) break;
+                    return fail("k_dropin_step finished without publishing word %d", which);
+                }
+                if (q != hipErrorNotReady) return fail("k_dropin_step: %s", hipGetErrorString(q));
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return 0;
+    }
+    // clear_dead right after a fast step: deferred; the step's launch already left what the getters
+    // and get_observation ask next.
+    int fast_clear_dead() {
+        defer_clear = true;
+        touch();
+        ro_prep_stale = true;
+        spec_ep = 0;
+        MFX_CHECK(take_info(pin_fast.p + fast_rec_clear, fast_rows));
+        obs_fast = true;
+        obs_ep = epoch;
+        return 0;
+    }
+
     int host_observe(int g, float** bufs) {
         if (!allocated) return fail("get_observation before reset");
         if (g < 0 || g >= n_groups()) return fail("get_observation: bad group %d", g);
@@ -1216,6 +1422,12 @@ public:
         if (n == 0) return 0;
         const TypeParams& T = gp.type[g];
         const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
+        if (obs_fast) {
+            MFX_CHECK(wait_fast(1));
+            memcpy(bufs[0], pin_fast.p + fast_view[g], sizeof(float) * n * VF);
+            memcpy(bufs[1], pin_fast.p + fast_feat[g], sizeof(float) * n * F);
+            return 0;
+        }
         if (obs_packed) {
             const float* hv = reinterpret_cast<const float*>(pin_obs.p) + obs_pack_off[g];
             memcpy(bufs[0], hv, sizeof(float) * n * VF);
@@ -1232,6 +1444,7 @@ public:
     int host_set_action(int g, const int* actions) {
         if (!allocated) return fail("set_action before reset");
         if (g < 0 || g >= n_groups()) return fail("set_action: bad group %d", g);
+        if (fast_dropin_ok()) return fast_set_action(g, actions);
         const int n = num_env0(g);
         const int rowcap = std::max(group_ub[g], 1);
         try {
@@ -1258,8 +1471,8 @@ public:
         return 0;
     }
     int host_step(int* done) {
-        const int keep_n = n_ep == epoch;
-        (void)keep_n;
+        if (!allocated) return fail("step before reset");
+        if (fast_dropin_ok()) return fast_step(done);
         MFX_CHECK(step(nullptr));
         MFX_CHECK(queue_info());                   // done + rewards / alive / positions in one transfer
         MFX_HIP(hipStreamSynchronize(stream));
@@ -1268,12 +1481,13 @@ public:
     }
     // clear_dead without a sync: with this epoch's alive flags at hand, the new group sizes are known.
     int host_clear_dead() {
+        if (spec_ep != 0 && spec_ep == epoch) return fast_clear_dead();
         const int G = n_groups();
         int nn[kMaxGroups] = {};
         const bool known = allocated && info_ep == epoch && n_ep == epoch;
         if (known)
             for (int g = 0; g < G; g++) {
-                const uint8_t* al = pin_info.p + info_off(g, kGetAlive);
+                const uint8_t* al = info_src + info_off(g, kGetAlive);
                 for (int i = 0; i < hn[g]; i++) nn[g] += al[i] != 0;
             }
         MFX_CHECK(clear_dead());
@@ -1286,7 +1500,7 @@ public:
         if (n == 0) return 0;
         if (what == kGetId || what == kGetReward || what == kGetPos || what == kGetAlive) {
             MFX_CHECK(ensure_info());
-            memcpy(out, pin_info.p + info_off(g, what), elem_bytes * n);
+            memcpy(out, info_src + info_off(g, what), elem_bytes * n);
             return 0;
         }
         const int rowcap = std::max(group_ub[g], 1);
@@ -1393,6 +1607,7 @@ public:
 
     int render() {                                // GridWorld::render + RenderGenerator::render_a_frame
         if (render_dir.empty()) return 0;
+        MFX_CHECK(flush_deferred());
         if (render_dir == "___debug___") return 0;   // the reference prints the map to stdout
         try {
             if (first_render) { start_recording(); gen_config(); }
@@ -1446,6 +1661,7 @@ public:
     }
 
     int mean_info(int group, float* out) {           // GridWorld.cc:832-853
+        MFX_CHECK(flush_deferred());
         const int n = num_env0(group), na = gtype(group).n_action;
         if (n == 0) return fail("mean_info of an empty group");          // the reference asserts
         std::vector<int> pos = group_pos(group), act((size_t)n);

@@ -44,6 +44,9 @@ hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int spli
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap);
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,
                               uint4* d_image, hipStream_t st);
+size_t dropin_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap, int rows);
+hipError_t launch_dropin_step(const GameParams& gp, const GameParams* d_gp, const State& s, const DropinArgs& da,
+                              hipStream_t st);
 hipError_t launch_get_env0(const GameParams* d_gp, const State& s, uint8_t* d_out, int rows, hipStream_t st);
 hipError_t launch_get(const GameParams* d_gp, const State& s, int g, int what, void* d_out, int rowcap,
                       hipStream_t st);

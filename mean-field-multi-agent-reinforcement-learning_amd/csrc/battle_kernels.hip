@@ -141,6 +141,7 @@ __device__ __forceinline__ EnvView global_view(const State& s, int e, int G) {
 #include "battle/step_core.inc"
 #include "battle/getters.inc"
 #include "battle/rollout.inc"
+#include "battle/dropin.inc"
 // ==================================================================================
 //  host-side launchers
 // ==================================================================================

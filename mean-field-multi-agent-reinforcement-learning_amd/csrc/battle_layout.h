@@ -136,6 +136,23 @@ struct State {                      // device pointers; every array is [E][strid
     int32_t* err;                   // [1] sticky device-side error code
     int32_t* ev;                    // [1 + 3 * acap] env 0's attack events of the last step (render):
                                     //   count, then (attacker id, target x, target y) in shuffle order
+    int serial_step;                // this step runs the serial forms: a group's set_action was called
+                                    //   more than once since the last step, so an agent may appear twice
+                                    //   in the action buffers (the parallel forms take one entry per agent)
+};
+
+// Arguments of the drop-in single-env step (k_dropin_step, battle/dropin.inc).
+struct DropinArgs {
+    const int32_t* acts[kMaxGroups];     // deferred set_action buffers (host-mapped), null: none
+    int n_acts[kMaxGroups];              //   and their lengths (group sizes after the deferred clear)
+    int pending_clear;                   // a clear_dead is deferred from the previous step
+    int rows;                            // rows per group of the records and observation blocks
+    uint8_t* rec_step;                   // record after the step          (host-mapped)
+    uint8_t* rec_clear;                  // record after the clear_dead    (host-mapped)
+    float* view[kMaxGroups];             // [rows][VH*VW*NC] per group     (host-mapped)
+    float* feat[kMaxGroups];             // [rows][F]
+    uint32_t* flag;                      // [2] host-mapped coherent words: seq once both records are
+    uint32_t seq;                        //   written, seq once the observation is
 };
 
 // Arguments of the fused rollout step (k_rollout): one launch = one step of the
@@ -147,7 +164,8 @@ struct RolloutArgs {
     int rowcap;                     // rows per env in every per-agent output (>= max group size)
     int32_t* actions;               // [E][G][rowcap]  actions taken this step
     float* rewards;                 // [E][G][rowcap]  get_reward after the step
-    double* mean_act;               // [E][G][n_action] former_act_prob (senario_battle.py:141)
+    double* mean_act;               // [E][G][mean_stride] former_act_prob (senario_battle.py:141); group g
+    int mean_stride;                //   fills its first n_action(g) entries; stride = max n_action
     float* ep_return;               // [E][G]  running episode return (sum of rewards)
     int32_t* ep_len;                // [E]     steps into the current episode
     double* stats;                  // [E][4]  finished episodes, sum final return g0, g1, kills

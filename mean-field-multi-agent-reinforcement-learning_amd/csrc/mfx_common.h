@@ -73,6 +73,22 @@ struct PinBuf {                    // grow-only pinned host buffer (async DMA ta
 };
 
 template <class T>
+struct MappedBuf {                 // grow-only pinned host buffer the device reads / writes in place
+    T* p = nullptr;                //   host address
+    T* d = nullptr;                //   the device's address of the same memory
+    size_t n = 0;
+    void ensure(size_t want, unsigned flags = 0) {
+        if (want <= n) return;
+        if (p) (void)hipHostFree(p);
+        p = d = nullptr;
+        MFX_HIP_THROW(hipHostMalloc((void**)&p, sizeof(T) * want, hipHostMallocMapped | flags));
+        MFX_HIP_THROW(hipHostGetDevicePointer((void**)&d, p, 0));
+        n = want;
+    }
+    ~MappedBuf() { if (p) (void)hipHostFree(p); }
+};
+
+template <class T>
 struct DevBuf {                    // grow-only device buffer
     T* p = nullptr;
     size_t n = 0;

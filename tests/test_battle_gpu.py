@@ -17,8 +17,12 @@ import common
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("fast", ["1", "0"])
 @pytest.mark.parametrize("name", ["battle40_seq", "battle40_s1", "battle40_s2", "battle64"])
-def test_hip_replays_reference_fixture(name):
+def test_hip_replays_reference_fixture(name, fast, monkeypatch):
+    """fast 1: the drop-in's one-launch step (k_dropin_step, deferred set_action / clear_dead);
+    0: the per-call path."""
+    monkeypatch.setenv("MFX_DROPIN_FAST", fast)
     assert common.replay_case(common.HIP_LIB, name) == []
 
 
@@ -78,11 +82,15 @@ def _random_scenario(lib_path, map_size, n0, n1, seed, steps, n_walls, episodes=
     return out
 
 
+@pytest.mark.parametrize("fast", ["1", "0"])
 @pytest.mark.parametrize("map_size,n0,n1,seed,walls", [
     (12, 5, 9, 1, 6), (20, 30, 30, 2, 20), (33, 60, 40, 3, 50), (64, 128, 128, 4, 0), (110, 300, 250, 5, 100),
     # envs too large for k_step's LDS copy: k_step_big (attack_big, band sort, move_jump) on random crowds
     (180, 1500, 1500, 6, 300), (256, 2500, 2000, 7, 600)])
-def test_hip_matches_oracle_random_scenarios(map_size, n0, n1, seed, walls):
+def test_hip_matches_oracle_random_scenarios(map_size, n0, n1, seed, walls, fast, monkeypatch):
+    monkeypatch.setenv("MFX_DROPIN_FAST", fast)
+    if fast == "0" and map_size > 110:
+        pytest.skip("the large maps never take the fast step")
     ref = _random_scenario(common.ORACLE_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
     got = _random_scenario(common.HIP_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
     assert len(got) == len(ref)
@@ -165,3 +173,75 @@ def test_render_frames_match_reference(tmp_path):
         assert (tmp_path / "hip" / f).read_bytes() == (tmp_path / "ref" / f).read_bytes(), f
     assert counts["hip"] == counts["ref"]
     assert any(len(c) for c in counts["ref"])
+
+
+def _odd_sequence(lib_path, seed):
+    """Call orders around the drop-in's deferred set_action / clear_dead: observation and getters
+    between step and clear_dead, a step without clear_dead, one group acting, set_action twice before
+    a step, get_info extras, a reset with a clear_dead pending.  Returns the SHA of every output."""
+    env, h = common.battle_env(lib_path, 24)
+    rs = np.random.RandomState(seed)
+    out = []
+
+    def rec(*arrs):
+        out.append(bd.sha(np.frombuffer(b"".join(np.ascontiguousarray(a).tobytes() for a in arrs), np.uint8)))
+
+    def obs():
+        for g in range(2):
+            v, f = env.get_observation(h[g])
+            rec(v, f, env.get_agent_id(h[g]))
+
+    def act(g):
+        n = env.get_num(h[g])
+        a = rs.randint(0, 21, size=n).astype(np.int32)
+        env.set_action(h[g], a)
+
+    def getters():
+        for g in range(2):
+            rec(env.get_reward(h[g]), env.get_alive(h[g]), env.get_pos(h[g]), env.get_agent_id(h[g]),
+                np.array([env.get_num(h[g])]))
+
+    left, right = bd.block_positions(24, 24)
+    for ep in range(2):
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        for t in range(40):
+            k = t % 8
+            obs()
+            if k == 3:
+                act(0)                                   # group 1 does not act this step
+            elif k == 5:
+                act(0); act(1); act(1)                   # group 1 sets its actions twice
+            else:
+                act(0); act(1)
+            rec(np.array([env.step()]))
+            getters()
+            if k == 2:
+                obs()                                    # before clear_dead: dead agents still listed
+            if k == 4:
+                rec(np.asarray(env._get_walls_info()), env.get_mean_info(h[0]), env.get_global_minimap(8, 8))
+                continue                                 # no clear_dead this step
+            if k == 6:
+                getters()
+            env.clear_dead()
+            if k == 7:
+                getters()
+            if ep == 0 and t == 25:
+                break                                    # reset with a clear_dead pending
+    del env
+    return out
+
+
+@pytest.mark.parametrize("fast", ["1", "0"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_dropin_odd_call_orders(seed, fast, monkeypatch):
+    """Against the reference engine itself (oracle/_ref): the extras are not in the C oracle."""
+    if not os.path.exists(common.REF_LIB):
+        pytest.skip("oracle/_ref not built")
+    monkeypatch.setenv("MFX_DROPIN_FAST", fast)
+    ref = _odd_sequence(common.REF_LIB, seed)
+    got = _odd_sequence(common.HIP_LIB, seed)
+    assert len(got) == len(ref)
+    first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
+    assert first_bad is None, "first divergence at record %s" % first_bad

@@ -414,3 +414,70 @@ def test_rollout_substeps_match_single_steps(sub):
         eng.sync()
         snaps.append((v, f))
     assert torch.equal(snaps[0][0], snaps[1][0]) and torch.equal(snaps[0][1], snaps[1][1])
+
+
+def _mixed_action_config(map_size):
+    """Battle rules where group 1 attacks only its 4 orthogonal neighbours: n_action 21 and 17, so the
+    [E][G][21] mean-action rows hold 17 entries for group 1 (stride = the largest n_action)."""
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": map_size, "map_height": map_size, "minimap_mode": True, "embedding_size": 10})
+    base = dict(width=1, length=1, hp=10, speed=2, view_range=gw.CircleRange(6), damage=2, step_recover=0.1,
+                step_reward=-0.005, kill_reward=5, dead_penalty=-0.1, attack_penalty=-0.1)
+    t0 = cfg.register_agent_type("wide", dict(base, attack_range=gw.CircleRange(1.5)))
+    t1 = cfg.register_agent_type("cross", dict(base, attack_range=gw.CircleRange(1)))
+    armies = [cfg.add_group(t0), cfg.add_group(t1)]
+    a, b = (gw.AgentSymbol(g, index="any") for g in armies)
+    cfg.add_reward_rule(gw.Event(a, "attack", b), receiver=a, value=0.2)
+    cfg.add_reward_rule(gw.Event(b, "attack", a), receiver=b, value=0.2)
+    return cfg
+
+
+def test_rollout_mixed_n_action_mean_rows():
+    """Groups with different n_action: every group's mean action lands in its own row of the
+    [E][G][max n_action] buffer (no overlap between groups or envs), checked against the oracle."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    map_size, n_side, E, T = 32, 40, 3, 30
+    cfg = _mixed_action_config(map_size)
+    probe = common.config_env(common.ORACLE_LIB, cfg, map_size)[0]
+    ph = probe.get_handles()
+    nas = [probe.get_action_space(h)[0] for h in ph]
+    assert nas == [21, 17], nas
+    del probe
+    left, right = bd.block_positions(map_size, n_side)
+    eng = BattleBatch(map_size, E, config=cfg, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=400, eps=0.3, seed=4, stagger=False)
+    rc, NA = eng.rowcap, 21
+    oracles = []
+    for e in range(E):
+        env, h = common.config_env(common.ORACLE_LIB, cfg, map_size)
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        oracles.append((env, h))
+    for t in range(T):
+        eng.rollout_step(1)
+        act = torch.empty(E * 2 * rc, dtype=torch.int32)
+        mean = torch.full((E * 2 * NA,), -7.0, dtype=torch.float64)
+        eng.rollout_copy("actions", act)
+        eng.rollout_copy("mean_action", mean)
+        eng.sync()
+        for e, (env, h) in enumerate(oracles):
+            acts = []
+            for g in range(2):
+                n = len(env.get_observation(h[g])[0])
+                a = act.numpy().reshape(E, 2, rc)[e, g, :n].astype(np.int32)
+                acts.append(a)
+                want = np.bincount(a, minlength=nas[g]) / n if n else np.full(nas[g], np.nan)
+                row = mean.numpy().reshape(E, 2, NA)[e, g]
+                assert np.array_equal(row[:nas[g]], want, equal_nan=True), (e, t, g)
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            env.clear_dead()
+            if done:
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
