@@ -5,7 +5,10 @@
  * examples/battle_model/src/runtime_api.h:118-181 (implemented at runtime_api.cc:15-169), so
  * the reference python wrapper examples/battle_model/python/magent/gridworld.py (ctypes, no
  * argtypes) and c_lib.py:13-31 bind this library unchanged.  Those calls act on env 0 and move
- * data through caller-owned host buffers, exactly like the reference.
+ * data through caller-owned host buffers, exactly like the reference.  On one env whose config the
+ * fused kernels take, set_action and clear_dead are deferred and env_step is ONE launch
+ * (k_dropin_step) that also leaves the getters' records and the next observation in host-mapped
+ * memory; any other call first runs the deferred work (MFX_DROPIN_FAST=0: one launch per call).
  *
  * Part 2 is this library's batched device API: E envs per engine, every buffer in HBM.
  * Part 3 covers the Ising lattice / tabular MF-Q (the reference's examples/ising_model and
@@ -33,8 +36,8 @@ int env_new_game(void **game, const char *name);
 /* runtime_api.h:119 */
 int env_delete_game(void *game);
 /* runtime_api.h:120 -- keys of GridWorld::set_config (GridWorld.cc:126-155): map_width,
- * map_height (int*), minimap_mode (bool*), embedding_size (int*), render_dir (char*),
- * seed (int*); food_mode / turn_mode / goal_mode must stay false */
+ * map_height (int*), minimap_mode, food_mode, turn_mode, goal_mode (bool*), embedding_size (int*),
+ * render_dir (char*), seed (int*) -- every key the reference accepts */
 int env_config_game(void *game, const char *key, void *value);
 /* runtime_api.h:123 */
 int env_reset(void *game);
@@ -47,9 +50,12 @@ int env_step(void *game, int *done);
 /* runtime_api.h:127 -- float[n] */
 int env_get_reward(void *game, int group, float *buffer);
 /* runtime_api.h:130 -- num, id, pos, alive, action_space, view_space, feature_space,
- * view2attack, attack_base, both_attack (GridWorld.cc:777-978) */
+ * view2attack, attack_base, both_attack, global_minimap, mean_info, walls_info,
+ * render_window_info, attack_event, groups_info (GridWorld.cc:777-978) */
 int env_get_info(void *game, int group, const char *name, void *buffer);
-/* runtime_api.h:133-134 -- rendering is out of scope: accepted, no-op */
+/* runtime_api.h:133-134 -- RenderGenerator's frame files: config.json + video_<n>.txt of env 0
+ * (RenderGenerator.cc), byte-identical to the reference build's; only the websocket server and the
+ * JS viewer are out of scope */
 int env_render(void *game);
 int env_render_next_file(void *game);
 /* runtime_api.h:140 -- AgentType reflection keys (AgentType.cc:63-101) */
@@ -61,12 +67,15 @@ int gridworld_add_agents(void *game, int group, int n, const char *method, const
                          const int *dir);
 /* runtime_api.h:146 */
 int gridworld_clear_dead(void *game);
-/* runtime_api.h:147 -- deprecated in the reference; returns -1 */
+/* runtime_api.h:147 -- "random" only (GridWorld.cc:729-740): advances the engine LCG like the
+ * reference, goals are never read back */
 int gridworld_set_goal(void *game, int group, const char *method, const int *linear_buffer);
-/* runtime_api.h:150-153 -- reward DSL.  Supported: rules triggered by one attack / kill /
- * collide event between 'any' agents of two groups, rewarding its subject and/or object.
- * The reference python passes 6 arguments to the 7-parameter add_reward_rule; auto_value is
- * never read (RewardEngine.cc:252 reads it for OP_ALIGN only). */
+/* runtime_api.h:150-153 -- the full reward DSL (RewardEngine.cc:14-443): and / or / not over
+ * attack / kill / collide / at / in / die / in_a_line events, 'any' / 'all' / fixed-index symbols,
+ * group receivers, terminal rules.  Rules of the one-event attack/kill/collide form run
+ * data-parallel, the rest through a one-lane interpreter; 'align' fails loudly (the reference
+ * never fills the counters it reads).  The reference python passes 6 arguments to the
+ * 7-parameter add_reward_rule; auto_value is never read (RewardEngine.cc:252, OP_ALIGN only). */
 int gridworld_define_agent_symbol(void *game, int no, int group, int index);
 int gridworld_define_event_node(void *game, int no, int op, int *inputs, int n_inputs);
 int gridworld_add_reward_rule(void *game, int on, int *receiver, float *value, int n_receiver, bool is_terminal,
