@@ -255,7 +255,8 @@ def main():
     eng = BattleBatch(args.map, E, stream=stream)
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     S = max(1, args.substeps)
-    eng.rollout_substeps(S)
+    if S != 1:
+        eng.rollout_substeps(S)
     grid, _ = eng.rollout_info()
     big = grid == E and args.map * args.map > 64 * 64     # k_observe_items + k_rollout_big (state in HBM)
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")

@@ -33,7 +33,10 @@ class BattleBatch:
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
                    "mfx_battle_rollout_copy_at"):
-            getattr(self._dll, fn).restype = ctypes.c_int
+            try:
+                getattr(self._dll, fn).restype = ctypes.c_int
+            except AttributeError:          # an older build of the library (A/B runs)
+                pass
         self._dll.mfx_last_error.restype = ctypes.c_char_p
         self.handles = self.env.get_handles()
         self.n_envs = n_envs
