@@ -35,7 +35,7 @@ extern "C" {
 // R replicas of an N-agent lattice whose neighbour table nbr[N][K] (ascending ids) comes from
 // Ising.py:_calc_mask (computed by the python Scenario).
 MFX_API int mfx_ising_create(int R, int N, int K, const int16_t* nbr, void** handle) {
-    if (R < 1 || N < 1 || N > 1024 || K < 1 || K > 16) return mfx::fail("ising: need 1 <= N <= 1024, 1 <= K <= 16");
+    if (R < 1 || N < 1 || N > 32767 || K < 1 || K > 16) return mfx::fail("ising: need 1 <= N <= 32767, 1 <= K <= 16");
     try {
         auto* e = new IsingEngine();
         e->R = R; e->N = N; e->K = K;

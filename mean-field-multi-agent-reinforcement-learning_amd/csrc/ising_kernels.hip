@@ -5,7 +5,8 @@
 // main_MFQ_Ising.py (:55-67 Boltzmann exploration, :103-159 episode loop).
 //
 // Layout: R independent replicas of an L x L periodic lattice, N = L*L agents, agent i at
-// row i / L, column i % L (Ising.py:81-90).  One workgroup per replica, one thread per spin.
+// row i / L, column i % L (Ising.py:81-90).  One workgroup per replica, one thread per spin (up
+// to 1024 spins, Q in registers), or 1024 threads over the spins with Q in HBM (k_ising_mfq_big).
 //   spins  u8  [R][N]        0 = down, 1 = up (global_state)
 //   nbr    i16 [N][K]        neighbour ids of agent i in ascending id order (spin_mask == 1)
 //   Q      f64 [R][N][K+1][2]
@@ -21,6 +22,7 @@
 namespace mfx {
 
 constexpr int kIsingMaxK = 16;
+constexpr int kIsingMaxN = 32767;      // int16 neighbour ids; 3 N bytes of LDS in k_ising_mfq_big
 
 // ------------------------------------------------------------------ env step
 // IsingMultiAgentEnv._step (environment.py:49-78): spin_i := action_i for every agent, then
@@ -30,7 +32,7 @@ __global__ void __launch_bounds__(1024) k_ising_step(int N, int K, const int16_t
                                                      uint8_t* __restrict__ spins, const int32_t* __restrict__ actions,
                                                      double* __restrict__ reward, uint8_t* __restrict__ obs,
                                                      int32_t* __restrict__ n_up, double* __restrict__ order) {
-    __shared__ uint8_t sp[4096];
+    extern __shared__ uint8_t sp[];                                   // [N] the new spins
     __shared__ int cnt;
     const int r = blockIdx.x;
     uint8_t* S = spins + (size_t)r * N;
@@ -167,16 +169,98 @@ __global__ void __launch_bounds__(1024) k_ising_mfq(IsingMfqArgs a) {
     if (i == 0 && a.steps_out) a.steps_out[r] = t;
 }
 
+// ------------------------------------------------------------------ fused MF-Q episode, large lattices
+// N > 1024 (up to kIsingMaxN): one 1024-lane workgroup per replica, lane l owns agents l, l + 1024, ...
+// The Q rows live in the output buffer (HBM, each row touched by its owner only) and the spins, the
+// new spins and the step's states in LDS (3 N bytes).  Same float64 operation sequence as k_ising_mfq.
+template <int KMAX>
+__global__ void __launch_bounds__(1024) k_ising_mfq_big(IsingMfqArgs a) {
+    extern __shared__ uint8_t lds[];
+    __shared__ int cnt[2];
+    const int r = blockIdx.x, N = a.N, K = a.K;
+    uint8_t* sp = lds;                 // spins before the step
+    uint8_t* nsp = lds + N;            // spins after the step (the actions)
+    uint8_t* stl = lds + 2 * N;        // each agent's state (up-neighbour count) this step
+    double* Q = a.q_out + (size_t)r * N * (K + 1) * 2;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        sp[i] = a.spins0[(size_t)r * N + i];
+        for (int k = 0; k < 2 * (K + 1); ++k) Q[(size_t)i * (K + 1) * 2 + k] = 0.0;
+    }
+    if (threadIdx.x == 0) { cnt[0] = 0; cnt[1] = 0; }
+    __syncthreads();
+    double current_t = 0.3, max_order = 0.0;
+    int done_ = 0, t = 0;
+    const int words = (N + 31) >> 5;
+    for (t = 0; t < a.T; ++t) {
+        if (t % a.decay_gap == 0) current_t *= a.decay_rate;           // main_MFQ_Ising.py:108-112
+        if (current_t < a.temperature) current_t = a.temperature;
+        for (int i = threadIdx.x; i < N; i += blockDim.x) {            // state + Boltzmann action (:55-67)
+            int st = 0;
+            for (int k = 0; k < K; ++k) st += sp[a.nbr[i * K + k]];
+            const double* qr = Q + ((size_t)i * (K + 1) + st) * 2;
+            const double q0 = qr[0], q1 = qr[1];
+            const double e0 = exp(q0 / current_t), e1 = exp(q1 / current_t);
+            const double denom = e0 + e1;
+            const double p0 = e0 / denom, p1 = e1 / denom;
+            const double c0 = p0 / (p0 + p1);
+            const double u = a.u ? a.u[((size_t)r * a.T + t) * N + i]
+                                 : philox_uniform(a.seed, (uint32_t)r, (uint32_t)t, (uint32_t)i);
+            nsp[i] = (u >= c0) ? 1 : 0;
+            stl[i] = (uint8_t)st;
+        }
+        const int par = t & 1;
+        if (threadIdx.x == 0) cnt[par] = 0;
+        __syncthreads();
+        int ups = 0;
+        for (int i = threadIdx.x; i < N; i += blockDim.x) {            // reward on the new spins, Q (:122-133)
+            const int act = nsp[i];
+            int sum = 0;
+            for (int k = 0; k < K; ++k) sum += nsp[a.nbr[i * K + k]] ? 1 : -1;
+            const double gi = act ? 1.0 : -1.0;
+            const double rew = -((-0.5 * gi) * (double)sum);
+            const bool upd = !a.mask || ((a.mask[((size_t)r * a.T + t) * words + (i >> 5)] >> (i & 31)) & 1u);
+            if (upd) {
+                double* q = Q + ((size_t)i * (K + 1) + stl[i]) * 2 + act;
+                *q = *q + a.lr * (rew - *q);
+            }
+            ups += act;
+        }
+        atomicAdd(&cnt[par], ups);
+        __syncthreads();
+        for (int i = threadIdx.x; i < N; i += blockDim.x) sp[i] = nsp[i];
+        const int n_up = cnt[par], n_down = N - n_up;
+        const double order = (double)(n_up > n_down ? n_up - n_down : n_down - n_up) / ((double)N + 0.0);
+        if (threadIdx.x == 0) {
+            if (a.order_out) a.order_out[(size_t)r * a.T + t] = order;
+            if (a.nup_out) a.nup_out[(size_t)r * a.T + t] = n_up;
+        }
+        if (order > max_order) max_order = order;                      // :138-156 (same on all lanes)
+        if (fabs(max_order - order) < 0.001) ++done_;
+        else done_ = 0;
+        __syncthreads();                                               // sp complete before the next step
+        if (done_ == 500 || t > a.T) { ++t; break; }
+    }
+    if (a.spins_out)
+        for (int i = threadIdx.x; i < N; i += blockDim.x) a.spins_out[(size_t)r * N + i] = sp[i];
+    if (threadIdx.x == 0 && a.steps_out) a.steps_out[r] = t;
+}
+
 hipError_t launch_ising_step(int R, int N, int K, const int16_t* nbr, uint8_t* spins, const int32_t* actions,
                              double* reward, uint8_t* obs, int32_t* n_up, double* order, hipStream_t st) {
-    if (N > 4096 || K > kIsingMaxK) return hipErrorInvalidValue;
+    if (N > kIsingMaxN || K > kIsingMaxK) return hipErrorInvalidValue;
     const int threads = N >= 1024 ? 1024 : ((N + 63) / 64) * 64;
-    k_ising_step<<<R, threads, 0, st>>>(N, K, nbr, spins, actions, reward, obs, n_up, order);
+    k_ising_step<<<R, threads, N, st>>>(N, K, nbr, spins, actions, reward, obs, n_up, order);
     return hipGetLastError();
 }
 
 hipError_t launch_ising_mfq(const IsingMfqArgs& a, int R, hipStream_t st) {
-    if (a.N > 1024 || a.K > kIsingMaxK) return hipErrorInvalidValue;
+    if (a.N > kIsingMaxN || a.K > kIsingMaxK) return hipErrorInvalidValue;
+    if (a.N > 1024) {                  // Q rows in HBM, spins in LDS
+        const size_t lds = 3 * (size_t)a.N;
+        if (a.K <= 4) k_ising_mfq_big<4><<<R, 1024, lds, st>>>(a);
+        else k_ising_mfq_big<kIsingMaxK><<<R, 1024, lds, st>>>(a);
+        return hipGetLastError();
+    }
     const int threads = ((a.N + 63) / 64) * 64;
     if (a.K <= 4)
         k_ising_mfq<4><<<R, threads, 0, st>>>(a);

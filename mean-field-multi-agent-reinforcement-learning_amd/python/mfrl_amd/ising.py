@@ -7,7 +7,10 @@
                                            makes (initial spins, Boltzmann uniforms, act_group);
 * ``run_mfq(...)``                      -- the whole MF-Q episode in ONE kernel launch per batch
                                            of replicas: bit-identical to main_MFQ_Ising.py in
-                                           'reference' mode, on-device Philox in 'philox' mode.
+                                           'reference' mode, on-device Philox in 'philox' mode;
+* ``run_mfq_episodes(...)``             -- main_MFQ_Ising.py -epi E: episodes in sequence on one
+                                           numpy stream.
+Lattices up to 32767 agents (181 x 181); above 1024 the Q table lives in HBM (k_ising_mfq_big).
 """
 import ctypes
 
@@ -21,6 +24,17 @@ def neighbour_table(n_agents, view=1):
     L = int(np.ceil(np.power(n_agents, 1.0 / 2)))
     if L * L != n_agents:
         raise ValueError("the Ising lattice needs a square number of agents")
+    if n_agents > 32767:
+        raise ValueError("the device lattice holds at most 32767 agents (int16 neighbour ids)")
+    if 2 * view < L:
+        # the mask's cross of +-1..view along the row and the column, wrapped: distinct cells when the
+        # view is under half the side, so the rows below equal the mask scan (vectorised for large N)
+        idx = np.arange(n_agents)
+        r, c = idx // L, idx % L
+        cols = []
+        for d in range(1, view + 1):
+            cols += [((r - d) % L) * L + c, ((r + d) % L) * L + c, r * L + (c - d) % L, r * L + (c + d) % L]
+        return np.ascontiguousarray(np.sort(np.stack(cols, 1), axis=1).astype(np.int16))
     out = []
     for i in range(n_agents):
         row, col = i // L, i % L
@@ -57,17 +71,7 @@ def reference_stream(seed, n_agents, steps, act_rate=1.0):
     for _ in range(n_agents):
         rs.choice(2)
     spins0 = np.array([rs.choice(2) for _ in range(n_agents)], dtype=np.uint8)
-    u = np.empty((steps, n_agents), dtype=np.float64)
-    words = (n_agents + 31) // 32
-    mask = np.zeros((steps, words), dtype=np.uint32)
-    k = int(act_rate * n_agents)
-    bits = np.zeros(words * 32, dtype=np.uint8)
-    for t in range(steps):
-        u[t] = rs.random_sample(n_agents)
-        grp = rs.choice(n_agents, k, replace=False)
-        bits[:] = 0
-        bits[grp] = 1
-        mask[t] = _pack_bits(bits, words)
+    u, mask = _draw_steps(rs, n_agents, steps, act_rate)
     return spins0, u, mask
 
 
@@ -130,6 +134,45 @@ class IsingLattice:
                                       ctypes.c_double(decay_rate), decay_gap, P(u), P(mask), ctypes.c_uint(seed),
                                       P(q), P(order), P(nup), P(done)), "mfx_ising_mfq_run")
         return {"q": q, "order": order, "n_up": nup, "steps": done, "spins": self.get_spins()}
+
+
+def _draw_steps(rs, n_agents, steps, act_rate):
+    """Per-step draws of main_MFQ_Ising.py from RandomState rs: N Boltzmann uniforms, the act_group."""
+    u = np.empty((steps, n_agents), dtype=np.float64)
+    words = (n_agents + 31) // 32
+    mask = np.zeros((steps, words), dtype=np.uint32)
+    k = int(act_rate * n_agents)
+    bits = np.zeros(words * 32, dtype=np.uint8)
+    for t in range(steps):
+        u[t] = rs.random_sample(n_agents)
+        grp = rs.choice(n_agents, k, replace=False)
+        bits[:] = 0
+        bits[grp] = 1
+        mask[t] = _pack_bits(bits, words)
+    return u, mask
+
+
+def run_mfq_episodes(n_agents=400, temperature=0.8, steps=10000, episodes=1, lr=0.1, act_rate=1.0, decay_rate=0.99,
+                     decay_gap=2000, seed=13):
+    """main_MFQ_Ising.py with -epi episodes (:84-159): one RandomState over the whole run; every episode
+    re-draws the spins (env.reset), restarts Q at zero and the temperature at 0.3, and runs until its
+    own early stop.  An episode that stops at step s has consumed s steps of draws, so the next
+    episode's stream is cut from the generator only after the device reports s."""
+    lat = IsingLattice(n_agents, 1)
+    rs = np.random.RandomState(seed)
+    for _ in range(n_agents):                       # make_world -> reset_world (discarded)
+        rs.choice(2)
+    out = []
+    for _ in range(episodes):
+        lat.set_spins(np.array([[rs.choice(2) for _ in range(n_agents)]], dtype=np.uint8))
+        ahead = np.random.RandomState()
+        ahead.set_state(rs.get_state())
+        u, mask = _draw_steps(ahead, n_agents, steps, act_rate)
+        res = lat.run_mfq(steps, temperature, lr, decay_rate, decay_gap, u=u[None],
+                          mask=mask[None] if act_rate != 1.0 else None)
+        _draw_steps(rs, n_agents, int(res["steps"][0]), act_rate)     # what the episode consumed
+        out.append(res)
+    return out
 
 
 def run_mfq(n_agents=400, temperature=0.8, steps=10000, lr=0.1, act_rate=1.0, decay_rate=0.99, decay_gap=2000,

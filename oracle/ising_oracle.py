@@ -4,7 +4,8 @@ cpu_baseline leg may use it; the product never does).
 Restates, in vectorised numpy of its own:
   * Ising.py:_calc_mask (:7-58)               -> neighbours()
   * IsingWorld.step + Scenario.reward/observation (core.py:99-125, Ising.py:101-119) -> env_step()
-  * main_MFQ_Ising.py's episode loop (:84-159) and its numpy RandomState draws -> mfq()
+  * main_MFQ_Ising.py's episode loop (:84-159) and its numpy RandomState draws -> mfq(),
+    mfq_episodes() (-epi E: episodes in sequence on one stream)
 Pinned bit-exactly against tests/golden/ising_*.npz, which make_ising_fixtures.py recorded by
 running the reference's own Scenario / IsingWorld code.
 """
@@ -38,6 +39,19 @@ def mfq(n_agents, temperature, steps, lr=0.1, act_rate=1.0, decay_rate=0.99, dec
     rs = np.random.RandomState(seed)
     for _ in range(n_agents):                  # make_world -> reset_world
         rs.choice(2)
+    return _episode(rs, n_agents, temperature, steps, lr, act_rate, decay_rate, decay_gap)
+
+
+def mfq_episodes(n_agents, temperature, steps, episodes, lr=0.1, act_rate=1.0, decay_rate=0.99, decay_gap=2000,
+                 seed=13):
+    """main_MFQ_Ising.py -epi: every episode on the same RandomState (:84-159)."""
+    rs = np.random.RandomState(seed)
+    for _ in range(n_agents):
+        rs.choice(2)
+    return [_episode(rs, n_agents, temperature, steps, lr, act_rate, decay_rate, decay_gap) for _ in range(episodes)]
+
+
+def _episode(rs, n_agents, temperature, steps, lr, act_rate, decay_rate, decay_gap):
     spins = np.array([rs.choice(2) for _ in range(n_agents)], dtype=np.int64)   # env.reset()
     nbr = neighbours(n_agents)
     K = nbr.shape[1]

@@ -116,6 +116,66 @@ def run(n_agents, temperature, steps, lr=0.1, act_rate=1.0, decay_rate=0.99, dec
     return out, stop
 
 
+def run_episodes(n_agents, temperature, steps, episodes, lr=0.1, act_rate=1.0, decay_rate=0.99, decay_gap=2000,
+                 seed=13):
+    """main_MFQ_Ising.py:11-159 with -epi episodes: for i_episode: env.reset(), Q := 0, current_t := 0.3,
+    the step loop until its own early stop; one np.random stream over the whole run."""
+    np.random.seed(seed)
+    sc = load_scenario()
+    world = sc.make_world(num_agents=n_agents, agent_view=1)
+    env = Env(sc, world)
+    n_actions = 2
+    out = {}
+    for ep in range(episodes):
+        obs = np.stack(env.reset())
+        spins0 = np.array([a.state.spin for a in world.agents], dtype=np.int8)
+        max_order, done_ = 0.0, 0
+        Q = np.zeros((n_agents, 5, n_actions))
+        current_t = 0.3
+        acts, orders, nups = [], [], []
+        stop = steps
+        for t in range(steps):
+            action = np.zeros(n_agents, dtype=np.int32)
+            if t % decay_gap == 0:
+                current_t *= decay_rate
+            if current_t < temperature:
+                current_t = temperature
+            for i in range(n_agents):
+                s = np.count_nonzero(obs[i] == 1)
+                vals = [np.exp(Q[i, s, k] / current_t) for k in range(n_actions)]
+                denom = 0
+                for v in vals:
+                    denom += v
+                action[i] = np.random.choice(n_actions, 1, p=[v / denom for v in vals])[0]
+            obs_, reward, done, order_param, ups, downs = env.step(np.expand_dims(action, axis=1))
+            obs_ = np.stack(obs_)
+            act_group = np.random.choice(n_agents, int(act_rate * n_agents), replace=False)
+            for i in act_group:
+                s = np.count_nonzero(obs[i] == 1)
+                Q[i, s, action[i]] = Q[i, s, action[i]] + lr * (reward[i][0] - Q[i, s, action[i]])
+            obs = obs_
+            acts.append(action.astype(np.int8))
+            orders.append(order_param)
+            nups.append(ups)
+            if order_param > max_order:
+                max_order = order_param
+            if abs(max_order - order_param) < 0.001:
+                done_ += 1
+            else:
+                done_ = 0
+            if done_ == 500 or t > steps:
+                stop = t + 1
+                break
+        p = "e%d_" % ep
+        out[p + "spins0"] = spins0
+        out[p + "actions"] = np.stack(acts)
+        out[p + "order"] = np.array(orders)
+        out[p + "n_up"] = np.array(nups, dtype=np.int32)
+        out[p + "q_final"] = Q
+        out[p + "stop"] = np.int32(stop)
+    return out
+
+
 def main():
     manifest = {"generator": "tests/golden/make_ising_fixtures.py",
                 "reference": "examples/ising_model/Ising.py + multiagent/core.py (imported); "
@@ -133,6 +193,13 @@ def main():
     manifest["cases"]["ising10_act05"] = {"n_agents": 100, "temperature": 0.8, "steps": 200, "stopped_after": stop,
                                           "lr": 0.1, "act_rate": 0.5, "seed": 13, "decay_rate": 0.99,
                                           "decay_gap": 2000}
+    # main_MFQ_Ising.py -epi 3 on a 4x4 lattice at tau 0.1: the first two episodes stop early (order
+    # parameter flat for 500 steps), so each episode's draws start where the previous stop left them
+    out = run_episodes(16, 0.1, 2000, 3)
+    np.savez_compressed(os.path.join(HERE, "ising4_epi3.npz"), **out)
+    manifest["episode_cases"] = {"ising4_epi3": {"n_agents": 16, "temperature": 0.1, "steps": 2000, "episodes": 3,
+                                                 "stops": [int(out["e%d_stop" % k]) for k in range(3)], "lr": 0.1,
+                                                 "act_rate": 1.0, "seed": 13, "decay_rate": 0.99, "decay_gap": 2000}}
     with open(os.path.join(HERE, "ising_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))

@@ -62,3 +62,20 @@ def test_dropin_examples_wins_over_a_namespace_examples(tmp_path):
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().startswith(common.PY_DIR), out.stdout
+
+
+def test_oracle_episodes_match_reference_fixture():
+    """main_MFQ_Ising.py -epi 3 (tests/golden/ising4_epi3.npz): the episodes run in sequence on one
+    numpy stream; the first two stop early, so the third starts from draws shifted by both stops."""
+    import ising_oracle
+    with open(os.path.join(common.GOLDEN, "ising_manifest.json")) as f:
+        c = json.load(f)["episode_cases"]["ising4_epi3"]
+    fx = np.load(os.path.join(common.GOLDEN, "ising4_epi3.npz"))
+    got = ising_oracle.mfq_episodes(c["n_agents"], c["temperature"], c["steps"], c["episodes"], seed=c["seed"])
+    for k, ep in enumerate(got):
+        p = "e%d_" % k
+        assert ep["steps"] == int(fx[p + "stop"]) == c["stops"][k]
+        np.testing.assert_array_equal(ep["actions"], fx[p + "actions"])
+        assert ep["order"].tobytes() == fx[p + "order"].tobytes()
+        np.testing.assert_array_equal(ep["n_up"], fx[p + "n_up"])
+        assert ep["q"].tobytes() == fx[p + "q_final"].tobytes()

@@ -113,3 +113,50 @@ def test_philox_mode_phases():
     assert last(cold).mean() > 0.25, last(cold)
     assert last(hot).mean() < 0.15, last(hot)
     assert last(cold).mean() > last(hot).mean() + 0.15
+
+
+def test_episodes_match_reference_fixture():
+    """main_MFQ_Ising.py -epi 3 on the device (run_mfq_episodes): each episode one launch, the next
+    episode's stream cut after the stop step the device reports (tests/golden/ising4_epi3.npz)."""
+    from mfrl_amd.ising import run_mfq_episodes
+    with open(os.path.join(common.GOLDEN, "ising_manifest.json")) as f:
+        c = json.load(f)["episode_cases"]["ising4_epi3"]
+    fx = np.load(os.path.join(common.GOLDEN, "ising4_epi3.npz"))
+    got = run_mfq_episodes(c["n_agents"], c["temperature"], c["steps"], c["episodes"], seed=c["seed"])
+    for k, ep in enumerate(got):
+        p = "e%d_" % k
+        T = int(fx[p + "stop"])
+        assert int(ep["steps"][0]) == T == c["stops"][k]
+        assert ep["order"][0, :T].tobytes() == fx[p + "order"].tobytes()
+        np.testing.assert_array_equal(ep["n_up"][0, :T], fx[p + "n_up"])
+        assert ep["q"][0].tobytes() == fx[p + "q_final"].tobytes()
+
+
+@pytest.mark.parametrize("n_agents,steps", [(1600, 60), (4096, 40), (16384, 12)])
+def test_large_lattice_mfq_matches_oracle(n_agents, steps):
+    """Lattices beyond one 1024-lane workgroup (k_ising_mfq_big: Q in HBM, spins in LDS) in reference
+    mode against the numpy oracle: every order parameter, n_up and the float64 Q table, bit for bit."""
+    from mfrl_amd.ising import run_mfq
+    got = run_mfq(n_agents, 0.8, steps, seed=21)
+    ref = ising_oracle.mfq(n_agents, 0.8, steps, seed=21)
+    assert int(got["steps"][0]) == ref["steps"]
+    assert got["order"][0, :ref["steps"]].tobytes() == ref["order"].tobytes()
+    np.testing.assert_array_equal(got["n_up"][0, :ref["steps"]], ref["n_up"])
+    assert got["q"][0].tobytes() == ref["q"].tobytes()
+
+
+def test_large_lattice_env_step_matches_oracle():
+    from mfrl_amd.ising import IsingLattice
+    rs = np.random.RandomState(8)
+    n, R = 32761, 2                                          # 181 x 181, the largest lattice
+    lat = IsingLattice(n, replicas=R)
+    nbr = ising_oracle.neighbours(n)
+    np.testing.assert_array_equal(lat.nbr, nbr)
+    lat.set_spins(rs.randint(0, 2, size=(R, n)))
+    acts = rs.randint(0, 2, size=(R, n))
+    rew, obs, nup, order = lat.step(acts)
+    for r in range(R):
+        s, rw, ob, nu, od = ising_oracle.env_step(None, nbr, acts[r])
+        assert rew[r].tobytes() == rw.tobytes()
+        np.testing.assert_array_equal(obs[r], ob)
+        assert nup[r] == nu and order[r] == od
