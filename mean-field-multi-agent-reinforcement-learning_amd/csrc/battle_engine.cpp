@@ -214,6 +214,8 @@ public:
     hipEvent_t ro_ev[kMaxSplit + 1] = {};
     State ro_sub_s[kMaxSplit];
     RolloutArgs ro_sub_ra[kMaxSplit];
+    int ro_sub_n[kMaxSplit] = {};            // envs of sub-batch k
+    int sub_envs(int k) const { return ro_sub_n[k]; }
     DevBuf<RolloutCtx> ro_sub_ctx;
     // observation/step pipeline (LDS-sized envs): k_rollout_obs on ro_str[0] observes every env
     // from one copy of the per-env state while k_rollout<.., kSplit> steps the same envs from it
@@ -261,9 +263,12 @@ public:
         if (q.obs_mm) { q.obs_mm += (size_t)e0 * G * 169; q.obs_info += (size_t)e0 * s.cap; }
         q.env_base = e0;
         if (q.big_sort) q.big_sort += (size_t)e0 * s.acap;
-        if (q.obs_items) {
-            q.obs_items += (size_t)e0 * G * ((ra.rowcap + ra.obs_item_rows - 1) / ra.obs_item_rows);
-            q.obs_cnt += 4 * k;
+        if (q.obs_items) {   // sub-batch k's lists: obs_lists x obs_list_stride items from (e0 + kXcds k) env slots
+            const size_t slots = (size_t)G * ((ra.rowcap + ra.obs_item_rows - 1) / ra.obs_item_rows);
+            q.obs_items += ((size_t)e0 + (size_t)kXcds * k) * slots;
+            q.obs_cnt += 2 * kXcds * kObsCntPad * k;
+            const int n = sub_envs(k);
+            q.obs_list_stride = (size_t)((n + ra.obs_lists - 1) / ra.obs_lists) * slots;
         }
         return q;
     }
@@ -1101,19 +1106,26 @@ public:
                     ra.obs_mm = ro_mm.p; ra.obs_info = ro_info.p;
                     const int R = kItemRows;
                     const size_t slots = (size_t)(ra.rowcap + R - 1) / R;
-                    ro_items.ensure(2 * (size_t)E * n_groups() * slots);
-                    ro_cnt.ensure(4 * kMaxSplit);
+                    // per sub-batch of n envs: obs_lists lists of ceil(n / obs_lists) envs' items each,
+                    // i.e. at most n + kXcds env slots
+                    const size_t par_stride = ((size_t)E + (size_t)kXcds * kMaxSplit) * n_groups() * slots;
+                    ro_items.ensure(2 * par_stride);
+                    ro_cnt.ensure(2 * kXcds * kObsCntPad * kMaxSplit);
+                    const char* xv = getenv("MFX_ITEM_XCD");        // A/B only: 0 = one shared list
+                    ra.obs_lists = xv && atoi(xv) == 0 ? 1 : kXcds;
                     ra.obs_items = ro_items.p; ra.obs_cnt = ro_cnt.p;
-                    ra.obs_par_stride = (size_t)E * n_groups() * slots; ra.obs_item_rows = R;
+                    ra.obs_par_stride = par_stride; ra.obs_item_rows = R;
                     MFX_HIP_THROW(observe_items_grid(gp, R, &ro_item_grid));
                     const char* gd = getenv("MFX_ITEM_GRID_DIV");   // sweeps only
                     ro_item_grid = std::max(1, ro_item_grid / (gd ? std::max(1, atoi(gd)) : kItemGridDiv));
+                    if (ro_item_grid >= kXcds) ro_item_grid -= ro_item_grid % kXcds;   // as many per XCD
                 }
                 const int K = std::min(ro_split, E);
                 ro_sub_ctx.ensure(K);
                 std::vector<RolloutCtx> subs(K);
                 for (int k = 0; k < K; k++) {
                     const int e0 = (int)((long long)E * k / K), e1 = (int)((long long)E * (k + 1) / K);
+                    ro_sub_n[k] = e1 - e0;
                     ro_sub_s[k] = sub_state(e0, e1 - e0);
                     ro_sub_ra[k] = sub_args(e0, k);
                     subs[k].s = ro_sub_s[k]; subs[k].ra = ro_sub_ra[k];
@@ -1167,7 +1179,8 @@ public:
             MFX_CHECK(sync_cells());
             const int K = std::min(ro_split, E);
             if (ra.obs_mm && ro_prep_stale) {
-                if (ra.obs_items) MFX_HIP(hipMemsetAsync(ro_cnt.p, 0, sizeof(int32_t) * 4 * kMaxSplit, stream));
+                if (ra.obs_items)
+                    MFX_HIP(hipMemsetAsync(ro_cnt.p, 0, sizeof(int32_t) * 2 * kXcds * kObsCntPad * kMaxSplit, stream));
                 for (int k = 0; k < K; k++)
                     MFX_HIP(launch_obs_prep(d_gp, ro_sub_s[k], ro_sub_ra[k], (int)(ra.step_index & 1), stream));
             }

@@ -191,16 +191,25 @@ struct RolloutArgs {
     float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and
     uint32_t* obs_info;             //   [E][cap] packed hp/max | group << 31 of the NEXT observation,
                                     //   computed once per env at the end of the step (obs_prep_env)
-    uint32_t* obs_items;            //   [2][E * G * item_slots] observation work items (env << 12 |
-                                    //   group << 10 | chunk) by step parity, filed by obs_file_items
-    int32_t* obs_cnt;               //   [2][2] per parity: items filed, items taken (k_observe_items)
+    uint32_t* obs_items;            //   [2][obs_lists][obs_list_stride] observation work items (env << 12 |
+                                    //   group << 10 | chunk) by step parity, filed by obs_file_items into
+                                    //   list e % obs_lists (one list per XCD: the items of an env are taken
+                                    //   by workgroups of one XCD, whose L2 then holds that env's cells)
+    int32_t* obs_cnt;               //   [2][obs_lists][kObsCntPad] per parity and list: items filed, items
+                                    //   taken (k_observe_items)
     size_t obs_par_stride;          //   items per parity region of obs_items
+    size_t obs_list_stride;         //   items per list
+    int obs_lists;                  //   1 or kXcds
     int obs_item_rows;              //   agents per item
     const uint4* wall_image;        // [H*W] u16 cells of that image with the agents removed: every
                                     // install rebuilds the cells from it plus the agents' positions, so
                                     // per-env cells are neither read nor written back (State::cells is
                                     // rebuilt on demand, BattleEngine::sync_cells)
 };
+
+// XCDs of the MI355X (workgroup i of a launch runs on XCD i % kXcds) and the int32 pad of one
+// item-list counter pair (its own 64-B line)
+constexpr int kXcds = 8, kObsCntPad = 16;
 
 // Everything k_rollout reads besides GameParams, resident in HBM (uploaded when it changes); the
 // kernel re-reads it per env through scalar loads instead of pinning ~80 SGPRs for the launch.
