@@ -80,6 +80,11 @@ int gridworld_define_agent_symbol(void *game, int no, int group, int index);
 int gridworld_define_event_node(void *game, int no, int op, int *inputs, int n_inputs);
 int gridworld_add_reward_rule(void *game, int on, int *receiver, float *value, int n_receiver, bool is_terminal,
                               bool auto_value);
+/* Extension of env_get_observation (runtime_api.h:124) for the drop-in python: the same views and
+ * features of env 0, as pointers into engine-owned pinned memory the drop-in step wrote them to (no
+ * copy); valid until the step after next or env_delete_game.  Returns 1 (nothing set) when the
+ * observation is not held that way -- call env_get_observation then. */
+int mfx_env_observation_view(void *game, int group, float **view, float **feature, int *n);
 
 /* ---------------------------------------------------------------- part 2: batched Battle */
 /* Before the first env_reset: make the engine hold n_envs identical envs. */

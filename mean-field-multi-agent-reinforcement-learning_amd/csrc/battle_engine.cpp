@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -163,14 +164,32 @@ public:
     bool defer_act[kMaxGroups] = {};         // group g's actions wait in pin_fact
     int defer_n[kMaxGroups] = {};
     bool defer_clear = false;                // clear_dead waits for the next k_dropin_step
-    uint64_t spec_ep = 0;                    // epoch at which rec_clear / the observation blocks apply
+    uint64_t spec_ep = 0;                    // epoch at which the step record / the observation blocks apply
     bool obs_fast = false;                   // the observation cache is pin_fast's blocks
-    MappedBuf<uint8_t> pin_fast;             // rec_step | rec_clear | per group view block, feature block
+    MappedBuf<uint8_t> pin_fast;             // rec_step | per group view block, feature block
     MappedBuf<int32_t> pin_fact;             // [G][fact_rows] deferred actions
     MappedBuf<uint32_t> pin_flag;            // [2] k_dropin_step's completion words (coherent)
-    uint32_t fast_seq = 0;                   // sequence number of the last k_dropin_step launch
+    uint32_t fast_seq = 0;                   // sequence number of the last k_dropin_step request
+    uint32_t obs_seq = 0;                    // the request whose observation the cache holds
+    // Resident server (engines on their own stream, MFX_DROPIN_RESIDENT != 0): one k_dropin_step launch
+    // keeps env 0 in LDS and answers every env.step() posted in the mailbox (battle_layout.h
+    // DropinMailbox) -- no launch, no install per step.  It leaves after a stop request (quiesce(),
+    // before anything else touches the stream or the state) or after res_idle_us without a request,
+    // and is relaunched by the next step.
+    bool res_enabled = env_flag("MFX_DROPIN_RESIDENT", true);
+    bool res_live = false;                   // a server was launched and not asked to stop
+    bool fast_res = false;                   // the last request went to the resident server
+    int res_relaunch = 0;                    // relaunches after an idle exit (statistics)
+    MappedBuf<DropinMailbox> mbox;
+    DropinArgs res_da{};                     // the arguments of the live server (relaunch)
+    static bool env_flag(const char* name, bool dflt) {
+        const char* v = getenv(name);
+        return v ? atoi(v) != 0 : dflt;
+    }
     size_t fast_rows = 0, fact_rows = 0;
-    size_t fast_rec_clear = 0, fast_view[kMaxGroups] = {}, fast_feat[kMaxGroups] = {};
+    size_t fast_rec = 0, fast_view[kMaxGroups] = {}, fast_feat[kMaxGroups] = {}, fast_set_bytes = 0;
+    std::vector<void*> retired;              // outgrown pin_fast blocks (views may outlive them), freed last
+    std::vector<uint8_t> clr_rec;            // the record after a deferred clear_dead (host-built)
     DevBuf<int> st_i32, st_xs, st_ys, st_dirs;
     DevBuf<uint8_t> st_u8;
     // fused rollout (bench / throughput path)
@@ -229,6 +248,13 @@ public:
     RolloutCtx ro_pipe_host[2] = {};
 
     ~BattleEngine() {
+        (void)quiesce();
+        for (void* p : retired) (void)hipHostFree(p);
+#ifdef MFX_STAMPS
+        if (hst_n)
+            fprintf(stderr, "[magent_amd stamps] fast_step host us: enter->posted %.2f posted->record %.2f record->return %.2f (%ld steps)\n",
+                    hst[0] / hst_n, hst[1] / hst_n, hst[2] / hst_n, hst_n);
+#endif
         for (auto& x : act_ev) if (x) (void)hipEventDestroy(x);
         release();
         for (auto& x : ro_str) if (x) (void)hipStreamDestroy(x);
@@ -326,6 +352,7 @@ public:
 
     // ------------------------------------------------------------------ config
     int set_config(const char* key, void* p) {
+        MFX_CHECK(quiesce());
         touch();
         if (!strcmp(key, "map_width")) W = *(int*)p;
         else if (!strcmp(key, "map_height")) H = *(int*)p;
@@ -349,6 +376,7 @@ public:
     }
 
     int register_type(const char* name, int n, const char** keys, const float* values) {
+        MFX_CHECK(quiesce());
         touch();
         if (types.count(name)) return fail("duplicated name of agent type: %s", name);
         AgentTypeSpec t;
@@ -398,6 +426,7 @@ public:
     }
 
     int new_group(const char* type_name, int* group) {
+        MFX_CHECK(quiesce());
         touch();
         if (!types.count(type_name)) return fail("invalid name of agent type in new_group: %s", type_name);
         if (n_groups() >= kMaxGroups) return fail("at most %d groups", kMaxGroups);
@@ -659,6 +688,7 @@ public:
     }
 
     void ensure_capacity(int need_ids, int need_actions) {
+        if ((need_ids > s.cap || need_actions > s.acap) && quiesce() != 0) throw HipFailure("resident server: stop failed");
         const int G = n_groups();
         if (need_ids > s.cap) {
             int nc = std::max(64, s.cap);
@@ -787,6 +817,7 @@ public:
     }
 
     int check_err() {
+        MFX_CHECK(quiesce());
         int32_t h = 0;
         MFX_HIP(hipMemcpyAsync(&h, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         MFX_HIP(hipStreamSynchronize(stream));
@@ -804,6 +835,7 @@ public:
 
     int report_err(int32_t h) {
         if (!h) return 0;
+        MFX_CHECK(quiesce());
         MFX_HIP(hipMemsetAsync(d_err, 0, sizeof(int32_t), stream));
         static const char* msg[] = {"", "", "agent capacity exceeded", "no blank position for random placement",
                                     "output row capacity smaller than the group", "invalid action id",
@@ -1288,7 +1320,19 @@ public:
         return dropin_smem_bytes(gp, s.cells_n, s.cap, s.acap, (int)fast_rows_now()) <= 160 * 1024;
     }
     // Run deferred set_action / clear_dead for real, in call order (clear_dead came first).
+    // Stop the resident server (if one may be running) and wait until it has left: its LDS image
+    // must not outlive a change made by anything else, and nothing else may wait behind it.
+    int quiesce() {
+        if (!res_live) return 0;
+        res_live = false;
+        DropinMailbox* mb = mbox.p;
+        mb->cmd = kDropinStop;
+        __atomic_store_n(&mb->req, ++fast_seq, __ATOMIC_RELEASE);
+        MFX_HIP(hipStreamSynchronize(stream));
+        return 0;
+    }
     int flush_deferred() {
+        MFX_CHECK(quiesce());
         bool acts = false;
         for (int g = 0; g < kMaxGroups; g++) acts |= defer_act[g];
         spec_ep = 0;
@@ -1320,7 +1364,7 @@ public:
                 MFX_CHECK(flush_deferred());
                 MFX_HIP_THROW(hipStreamSynchronize(stream));
                 fact_rows = std::max(fact_rows, rows);
-                pin_fact.ensure((size_t)n_groups() * fact_rows);
+                pin_fact.ensure((size_t)n_groups() * fact_rows, hipHostMallocCoherent);
             }
             pending_ub += group_ub[g];
             ensure_capacity(0, pending_ub);
@@ -1339,7 +1383,16 @@ public:
         return 0;
     }
     // env.step(): one k_dropin_step launch and one sync.
+#ifdef MFX_STAMPS
+    // diagnostic build: host-side split of env.step() (enter -> request posted -> record seen -> return)
+    double hst[3] = {0, 0, 0};
+    long hst_n = 0;
+    std::chrono::steady_clock::time_point hst_t0, hst_t1;
+#endif
     int fast_step(int* done) {
+#ifdef MFX_STAMPS
+        hst_t0 = std::chrono::steady_clock::now();
+#endif
         touch();
         ro_prep_stale = true;
         MFX_CHECK(sync_cells());
@@ -1348,24 +1401,34 @@ public:
         DropinArgs da{};
         try {
             const size_t rec = (64 + (size_t)G * (((rows * kInfoRowBytes) + 15) & ~(size_t)15) + 255) & ~(size_t)255;
-            const size_t rec_clear = rec;
-            size_t off = 2 * rec;
+            // rec | observation set 0 | set 1: request k writes set k & 1, so the arrays a caller got
+            // from get_observation (mfx_env_observation_view) stay intact through the next step
+            size_t off = rec;
             size_t vo[kMaxGroups], fo[kMaxGroups];
             for (int g = 0; g < G; g++) {
                 const TypeParams& T = gp.type[g];
                 vo[g] = off; off = (off + rows * T.view_w * T.view_h * gp.n_ch * 4 + 255) & ~(size_t)255;
                 fo[g] = off; off = (off + rows * gp.feat_size[g] * 4 + 255) & ~(size_t)255;
             }
-            if (pin_fast.n < off) {
+            const size_t set_bytes = off - rec;
+            off += set_bytes;
+            if (pin_fast.n < off || (res_live && (int)rows != res_da.rows)) {
+                if (quiesce() != 0) throw HipFailure("quiesce failed");
                 MFX_HIP_THROW(hipStreamSynchronize(stream));   // the last launch may still write it
-                pin_fast.ensure(off);
+                if (pin_fast.n < off && pin_fast.p) {           // callers may still hold views of it
+                    retired.push_back(pin_fast.p);
+                    pin_fast.p = pin_fast.d = nullptr;
+                    pin_fast.n = 0;
+                }
+                pin_fast.ensure(off, hipHostMallocCoherent);
             }
+            fast_set_bytes = set_bytes;
             if (!pin_flag.p) {
                 pin_flag.ensure(2, hipHostMallocCoherent);
                 pin_flag.p[0] = pin_flag.p[1] = 0;
             }
             fast_rows = rows;
-            fast_rec_clear = rec_clear;
+            fast_rec = rec;
             for (int g = 0; g < G; g++) { fast_view[g] = vo[g]; fast_feat[g] = fo[g]; }
         } catch (const HipFailure& f) {
             return fail("%s", f.what());
@@ -1377,34 +1440,90 @@ public:
             da.feat[g] = reinterpret_cast<float*>(pin_fast.d + fast_feat[g]);
         }
         da.pending_clear = defer_clear;
+        da.obs_alt = fast_set_bytes / sizeof(float);
         da.rows = (int)rows;
         da.rec_step = pin_fast.d;
-        da.rec_clear = pin_fast.d + fast_rec_clear;
         da.flag = pin_flag.d;
-        da.seq = ++fast_seq;
         begin_step();
-        const hipError_t le = launch_dropin_step(gp, d_gp, s, da, stream);
+        fast_res = res_enabled && own_stream && !s.serial_step;
+        if (fast_res) {
+            if (!mbox.p) {
+                try { mbox.ensure(1, hipHostMallocCoherent); } catch (const HipFailure& f) { return fail("%s", f.what()); }
+                memset(mbox.p, 0, sizeof(DropinMailbox));
+            }
+            DropinMailbox* mb = mbox.p;
+            mb->cmd = kDropinStep;
+            mb->pending_clear = defer_clear;
+            for (int g = 0; g < kMaxGroups; g++) mb->n_acts[g] = g < G && defer_act[g] ? defer_n[g] : -1;
+            const uint32_t seq = ++fast_seq;
+            __atomic_store_n(&mb->req, seq, __ATOMIC_RELEASE);
+            if (!res_live) {
+                for (int g = 0; g < G; g++) da.acts[g] = pin_fact.d + (size_t)g * fact_rows;
+                da.mb = mbox.d;
+                da.seq = seq - 1;
+                da.idle = res_idle_ticks();
+                da.variant = res_variant();
+                res_da = da;
+                MFX_HIP(launch_dropin_step(gp, d_gp, s, da, stream));
+                res_live = true;
+            }
+        } else {
+            MFX_CHECK(quiesce());
+            da.seq = ++fast_seq;
+            const hipError_t le = launch_dropin_step(gp, d_gp, s, da, stream);
+            MFX_HIP(le);
+        }
         s.serial_step = 0;
-        MFX_HIP(le);
-        MFX_CHECK(wait_fast(0));                  // the records; the observation is still being written
+        obs_seq = fast_seq;
+#ifdef MFX_STAMPS
+        hst_t1 = std::chrono::steady_clock::now();
+#endif
+        MFX_CHECK(wait_fast(0, fast_seq));        // the records; the observation is still being written
+#ifdef MFX_STAMPS
+        const auto hst_t2 = std::chrono::steady_clock::now();
+#endif
         defer_clear = false;
         for (int g = 0; g < kMaxGroups; g++) defer_act[g] = false;
         pending_ub = 0;
         MFX_CHECK(take_info(pin_fast.p, rows));
         *done = info_hdr()[kMaxGroups + 1];
         spec_ep = epoch;
+#ifdef MFX_STAMPS
+        const auto hst_t3 = std::chrono::steady_clock::now();
+        hst[0] += std::chrono::duration<double, std::micro>(hst_t1 - hst_t0).count();
+        hst[1] += std::chrono::duration<double, std::micro>(hst_t2 - hst_t1).count();
+        hst[2] += std::chrono::duration<double, std::micro>(hst_t3 - hst_t2).count();
+        hst_n++;
+#endif
         return 0;
     }
-    // Spin on k_dropin_step's completion word `which` (0 records, 1 observation) of launch fast_seq.
-    // The stream is polled now and then, so a failed or faulted launch is reported instead of awaited.
-    int wait_fast(int which) {
-        volatile uint32_t* f = pin_flag.p + which;
-        for (uint32_t k = 1;; k++) {
-            if (*f == fast_seq) break;
-            if ((k & 255) == 0) {
+    // Spin on k_dropin_step's completion word `which` (0 records, 1 observation) of request `seq`.
+    // The stream is polled now and then, so a failed or faulted launch is reported instead of awaited;
+    // a resident server that left on its idle timeout before seeing the request is launched again.
+    int wait_fast(int which, uint32_t seq) {
+        const bool res = fast_res;
+        volatile uint32_t* f = res ? &mbox.p->done[which] : pin_flag.p + which;
+        // the stream is queried every ~100 us of waiting (a query costs microseconds; polling it by
+        // iteration count delayed the detection of the word)
+        const auto t_start = std::chrono::steady_clock::now();
+        auto t_next = t_start + std::chrono::microseconds(100);
+        for (uint32_t k = 1, relaunched = 0;; k++) {
+            if (*f == seq) break;
+            if ((k & 63) == 0 && std::chrono::steady_clock::now() >= t_next) {
+                t_next = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
+                if (t_next - t_start > std::chrono::seconds(20))
+                    return fail("k_dropin_step: request %u unanswered after 20 s (word %d = %u)", seq, which, *f);
                 const hipError_t q = hipStreamQuery(stream);
                 if (q == hipSuccess) {
-                    if (*f == fast_seq) break;
+                    if (*f == seq) break;
+                    if (res && res_live && seq == fast_seq && relaunched < 2) {
+                        DropinArgs da = res_da;      // the request is still posted: serve it
+                        da.seq = seq - 1;
+                        MFX_HIP(launch_dropin_step(gp, d_gp, s, da, stream));
+                        relaunched++;
+                        res_relaunch++;
+                        continue;
+                    }
                     return fail("k_dropin_step finished without publishing word %d", which);
                 }
                 if (q != hipErrorNotReady) return fail("k_dropin_step: %s", hipGetErrorString(q));
@@ -1414,6 +1533,19 @@ public:
         std::atomic_thread_fence(std::memory_order_acquire);
         return 0;
     }
+    static int res_variant() {
+        static const int v = getenv("MFX_DROPIN_VARIANT") ? atoi(getenv("MFX_DROPIN_VARIANT")) : 0;
+        return v;
+    }
+    unsigned long long res_idle_ticks() const {
+        int dev = 0, khz = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+            khz <= 0)
+            khz = 100000;                                  // gfx9: 100 MHz
+        const char* v = getenv("MFX_DROPIN_IDLE_US");
+        const long long us = v ? std::max(1, atoi(v)) : 2000;
+        return (unsigned long long)us * (unsigned long long)khz / 1000ull;
+    }
     // clear_dead right after a fast step: deferred; the step's launch already left what the getters
     // and get_observation ask next.
     int fast_clear_dead() {
@@ -1421,7 +1553,36 @@ public:
         touch();
         ro_prep_stale = true;
         spec_ep = 0;
-        MFX_CHECK(take_info(pin_fast.p + fast_rec_clear, fast_rows));
+        // the record after clear_dead, from the step's record (clear_dead_env): the alive rows in
+        // order, reward = next_r + group reward = step_reward + 0
+        const size_t rows = fast_rows, region = ((rows * kInfoRowBytes) + 15) & ~(size_t)15;
+        clr_rec.resize(fast_rec);
+        const uint8_t* src = pin_fast.p;
+        uint8_t* dst = clr_rec.data();
+        memcpy(dst, src, 64);
+        int32_t* hdr = reinterpret_cast<int32_t*>(dst);
+        for (int g = 0; g < n_groups(); g++) {
+            const int n = std::min(hdr[g], (int)rows);
+            const uint8_t* b = src + 64 + (size_t)g * region;
+            uint8_t* o = dst + 64 + (size_t)g * region;
+            const int32_t* ids = reinterpret_cast<const int32_t*>(b);
+            const int32_t* pos = reinterpret_cast<const int32_t*>(b + rows * 8);
+            const uint8_t* alive = b + rows * 16;
+            int32_t* oids = reinterpret_cast<int32_t*>(o);
+            float* orew = reinterpret_cast<float*>(o + rows * 4);
+            int32_t* opos = reinterpret_cast<int32_t*>(o + rows * 8);
+            uint8_t* oalive = o + rows * 16;
+            volatile float zero = 0.0f;
+            const float r = gp.type[g].step_reward + zero;
+            int k = 0;
+            for (int i = 0; i < n; i++) {
+                if (!alive[i]) continue;
+                oids[k] = ids[i]; orew[k] = r; opos[2 * k] = pos[2 * i]; opos[2 * k + 1] = pos[2 * i + 1]; oalive[k] = 1;
+                k++;
+            }
+            hdr[g] = k;
+        }
+        MFX_CHECK(take_info(dst, rows));
         obs_fast = true;
         obs_ep = epoch;
         return 0;
@@ -1436,9 +1597,10 @@ public:
         const TypeParams& T = gp.type[g];
         const size_t VF = (size_t)T.view_w * T.view_h * gp.n_ch, F = gp.feat_size[g];
         if (obs_fast) {
-            MFX_CHECK(wait_fast(1));
-            memcpy(bufs[0], pin_fast.p + fast_view[g], sizeof(float) * n * VF);
-            memcpy(bufs[1], pin_fast.p + fast_feat[g], sizeof(float) * n * F);
+            MFX_CHECK(wait_fast(1, obs_seq));
+            const size_t o = (obs_seq & 1) ? fast_set_bytes : 0;
+            memcpy(bufs[0], pin_fast.p + o + fast_view[g], sizeof(float) * n * VF);
+            memcpy(bufs[1], pin_fast.p + o + fast_feat[g], sizeof(float) * n * F);
             return 0;
         }
         if (obs_packed) {
@@ -1450,6 +1612,22 @@ public:
         const uint8_t* hv = pin_obs.p + obs_off_view(g);
         memcpy(bufs[0], hv, sizeof(float) * n * VF);
         memcpy(bufs[1], hv + sizeof(float) * obs_rows * VF, sizeof(float) * n * F);
+        return 0;
+    }
+    // get_observation without the copy: host pointers to env 0's observation of group g, written by
+    // the drop-in step into pinned memory (the set of the last request; the next request writes the
+    // other set, so they stay valid until the step after next).  1: not available (the caller copies
+    // through host_observe).
+    int observation_view(int g, float** view, float** feat, int* n) {
+        if (!allocated) return fail("get_observation before reset");
+        if (g < 0 || g >= n_groups()) return fail("get_observation: bad group %d", g);
+        MFX_CHECK(ensure_obs());
+        if (!obs_fast) return 1;
+        MFX_CHECK(wait_fast(1, obs_seq));
+        const size_t o = (obs_seq & 1) ? fast_set_bytes : 0;
+        *view = reinterpret_cast<float*>(pin_fast.p + o + fast_view[g]);
+        *feat = reinterpret_cast<float*>(pin_fast.p + o + fast_feat[g]);
+        *n = hn[g];
         return 0;
     }
     // No sync: the actions go out of pinned memory (one region per group, reused once the previous
@@ -1783,6 +1961,12 @@ MFX_API int env_delete_game(void* game) { delete MFX_ENV(game); return 0; }
 MFX_API int env_config_game(void* game, const char* name, void* value) { MFX_GUARD(MFX_ENV(game)->set_config(name, value)); }
 MFX_API int env_reset(void* game) { MFX_GUARD(MFX_ENV(game)->reset()); }
 MFX_API int env_get_observation(void* game, int group, float** buffer) { MFX_GUARD(MFX_ENV(game)->host_observe(group, buffer)); }
+// get_observation without the copy (the drop-in fast step): pointers to env 0's observation of the
+// group in engine-owned pinned memory, valid until the step after next or the engine's deletion.
+// Returns 1 when the observation is not held that way (use env_get_observation).
+MFX_API int mfx_env_observation_view(void* game, int group, float** view, float** feature, int* n) {
+    MFX_GUARD(MFX_ENV(game)->observation_view(group, view, feature, n));
+}
 MFX_API int env_set_action(void* game, int group, const int* actions) { MFX_GUARD(MFX_ENV(game)->host_set_action(group, actions)); }
 MFX_API int env_step(void* game, int* done) { MFX_GUARD(MFX_ENV(game)->host_step(done)); }
 MFX_API int env_get_reward(void* game, int group, float* buffer) {
@@ -1849,6 +2033,7 @@ MFX_API int mfx_battle_set_num_envs(void* game, int n_envs) {
 }
 MFX_API int mfx_battle_set_stream(void* game, void* stream) {
     BattleEngine* e = MFX_ENV(game);
+    MFX_CHECK(e->quiesce());
     if (e->own_stream && e->stream) { (void)hipStreamSynchronize(e->stream); (void)hipStreamDestroy(e->stream); }
     e->stream = (hipStream_t)stream;
     e->own_stream = false;
@@ -1869,6 +2054,7 @@ MFX_API int mfx_battle_clear_dead(void* game) { MFX_GUARD(MFX_ENV(game)->clear_d
 MFX_API int mfx_battle_sync(void* game) {
     BattleEngine* e = MFX_ENV(game);
     if (!e->allocated) return 0;
+    MFX_CHECK(e->quiesce());
     MFX_HIP(hipStreamSynchronize(e->stream));
     return e->check_err();
 }

@@ -47,7 +47,16 @@ constexpr int kStampW = 32;                  // stamps per env row
         __syncthreads();                                                                    \
         if (TID == 0 && g_stamps && (row) >= 0) g_stamps[(row) * kStampW + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// drop-in server: lane 0's clock at the phase boundaries of request `seq` (no extra barrier)
+#define MFX_DSTAMP(seq, i)                                                                  \
+    do {                                                                                    \
+        if (TID == 0 && g_stamps) {                                                         \
+            g_stamps[((seq) & 1023u) * kStampW + (i)] = __builtin_amdgcn_s_memtime();       \
+            g_stamps[((seq) & 1023u) * kStampW + 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                   \
+    } while (0)
 #else
+#define MFX_DSTAMP(seq, i) do {} while (0)
 #define MFX_STAMP(i) do {} while (0)
 #define MFX_TSTAMP(kW, i) do {} while (0)
 #define MFX_BSTAMP(row, i) do {} while (0)

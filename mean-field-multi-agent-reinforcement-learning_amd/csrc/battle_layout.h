@@ -142,17 +142,43 @@ struct State {                      // device pointers; every array is [E][strid
 };
 
 // Arguments of the drop-in single-env step (k_dropin_step, battle/dropin.inc).
+// The resident drop-in server's mailbox (k_dropin_step with DropinArgs::mb set), in coherent host
+// memory.  The host writes a request's fields, then `req` (release); the kernel answers in `done`,
+// on its own 128-B line so that the two sides do not write one line.
+enum : int32_t { kDropinStop = 0, kDropinStep = 1 };
+struct DropinMailbox {
+    uint32_t req;                        // sequence number of the latest request
+    int32_t cmd;                         // kDropinStep / kDropinStop
+    int32_t pending_clear;               // a clear_dead is deferred from the previous step
+    int32_t n_acts[kMaxGroups];          // deferred set_action lengths, -1: no call for the group
+    int32_t pad0[32 - 3 - kMaxGroups];
+    uint32_t done[4];                    // [0] records written, [1] observation written, [2] unused,
+                                         // [3] the kernel has left (the last request it saw)
+    int32_t pad1[28];
+};
+
 struct DropinArgs {
     const int32_t* acts[kMaxGroups];     // deferred set_action buffers (host-mapped), null: none
     int n_acts[kMaxGroups];              //   and their lengths (group sizes after the deferred clear)
     int pending_clear;                   // a clear_dead is deferred from the previous step
     int rows;                            // rows per group of the records and observation blocks
     uint8_t* rec_step;                   // record after the step          (host-mapped)
-    uint8_t* rec_clear;                  // record after the clear_dead    (host-mapped)
-    float* view[kMaxGroups];             // [rows][VH*VW*NC] per group     (host-mapped)
+    float* view[kMaxGroups];             // [rows][VH*VW*NC] per group     (host-mapped), set 0
     float* feat[kMaxGroups];             // [rows][F]
-    uint32_t* flag;                      // [2] host-mapped coherent words: seq once both records are
+    size_t obs_alt;                      // floats from set 0 to set 1: request seq writes set seq & 1
+    uint32_t* flag;                      // [2] host-mapped coherent words: seq once the record is
     uint32_t seq;                        //   written, seq once the observation is
+    // resident server (mb != null): the launch installs env 0 once and then answers every request
+    // posted in mb (acts[g] fixed, lengths and the clear flag from the mailbox, completion words
+    // mb->done) until a kDropinStop request or `idle` wall-clock ticks without one.  seq = the last
+    // request already answered; flag is unused.
+    DropinMailbox* mb;
+    unsigned long long idle;
+    int variant;                         // diagnostics (MFX_DROPIN_VARIANT): bit 0 polls without sleeping,
+                                         // bit 1 answers requests without doing the step (timing only),
+                                         // bit 3 writes the record in system-scope stores and publishes
+                                         // it without the system fence, bit 4 reads the actions with
+                                         // system-scope loads instead of an acquire fence
 };
 
 // Arguments of the fused rollout step (k_rollout): one launch = one step of the

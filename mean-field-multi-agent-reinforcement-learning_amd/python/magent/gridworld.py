@@ -12,7 +12,7 @@ import os
 
 import numpy as np
 
-from .c_lib import get_lib, as_float_c_array, as_int32_c_array
+from .c_lib import EngineError, get_lib, as_float_c_array, as_int32_c_array
 from .environment import Environment
 
 _CONFIG_TYPES = {
@@ -75,6 +75,12 @@ class GridWorld(Environment):
             self.group_handles.append(handle)
 
         self._init_obs_buf()
+        # engines that hold the drop-in step's observation in pinned memory hand it out without a copy
+        self._obs_view = getattr(L.dll, "mfx_env_observation_view", None) if hasattr(L, "dll") else None
+        if self._obs_view is not None:
+            fp = ctypes.POINTER(ctypes.POINTER(ctypes.c_float))
+            self._obs_view.argtypes = [ctypes.c_void_p, ctypes.c_int, fp, fp, ctypes.POINTER(ctypes.c_int32)]
+            self._obs_view.restype = ctypes.c_int
         self.view_space, self.feature_space, self.action_space = {}, {}, {}
         buf = np.empty((3,), dtype=np.int32)
         for h in self.group_handles:
@@ -137,9 +143,33 @@ class GridWorld(Environment):
             ret = bufs[group] = np.empty(shape=shape, dtype=dtype)
         return ret
 
+    def _pinned(self, ptr, shape):
+        """float32 array over engine-owned memory; it keeps this env (and so the memory) alive."""
+        count = 1
+        for d in shape:
+            count *= d
+        if count == 0:
+            return np.empty(shape, dtype=np.float32)
+        buf = (ctypes.c_float * count).from_address(ctypes.addressof(ptr.contents))
+        buf._owner = self
+        return np.frombuffer(buf, dtype=np.float32).reshape(shape)
+
     def get_observation(self, handle):
-        """(views [n, H, W, C] float32, features [n, F] float32) of every agent of the group."""
+        """(views [n, H, W, C] float32, features [n, F] float32) of every agent of the group.
+
+        After a drop-in step the engine already holds them in pinned memory and the arrays are views
+        of it (no copy); like the reference's reused buffers they are overwritten later -- here by the
+        step after next, which leaves them valid through the replay push that follows env.step()."""
         g = _hv(handle)
+        if self._obs_view is not None:
+            vp, fp, n = ctypes.POINTER(ctypes.c_float)(), ctypes.POINTER(ctypes.c_float)(), ctypes.c_int32()
+            r = self._obs_view(self.game, g, ctypes.byref(vp), ctypes.byref(fp), ctypes.byref(n))
+            if r == 0:
+                n = n.value
+                return self._pinned(vp, (n,) + self.view_space[g]), self._pinned(fp, (n,) + self.feature_space[g])
+            if r < 0:
+                raise EngineError("mfx_env_observation_view failed (%d): %s"
+                                  % (r, self._lib.dll.mfx_last_error().decode()))
         n = self.get_num(handle)
         view = self._get_obs_buf(g, self.OBS_INDEX_VIEW, (n,) + self.view_space[g], np.float32)
         feat = self._get_obs_buf(g, self.OBS_INDEX_HP, (n,) + self.feature_space[g], np.float32)
