@@ -174,11 +174,10 @@ struct DropinArgs {
     // request already answered; flag is unused.
     DropinMailbox* mb;
     unsigned long long idle;
-    int variant;                         // diagnostics (MFX_DROPIN_VARIANT): bit 0 polls without sleeping,
-                                         // bit 1 answers requests without doing the step (timing only),
+    int variant;                         // diagnostics (MFX_DROPIN_VARIANT): bit 1 answers requests
+                                         // without doing the step (timing only),
                                          // bit 3 writes the record in system-scope stores and publishes
-                                         // it without the system fence, bit 4 reads the actions with
-                                         // system-scope loads instead of an acquire fence
+                                         // it without the system fence
 };
 
 // Arguments of the fused rollout step (k_rollout): one launch = one step of the
