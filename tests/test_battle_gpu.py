@@ -245,3 +245,56 @@ def test_dropin_odd_call_orders(seed, fast, monkeypatch):
     assert len(got) == len(ref)
     first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
     assert first_bad is None, "first divergence at record %s" % first_bad
+
+
+@pytest.mark.parametrize("mode", ["resident_idle_exits", "one_launch_per_step"])
+def test_dropin_resident_server_modes(mode, monkeypatch):
+    """The resident drop-in server (one k_dropin_step launch answering env.step() through a mailbox)
+    with an idle timeout of 20 us, so that it leaves between nearly every pair of steps and is
+    relaunched with the request already posted (the relaunch race); and the one-launch-per-step form
+    (MFX_DROPIN_RESIDENT=0).  Both against the C oracle, two episodes with walls and random placement."""
+    monkeypatch.setenv("MFX_DROPIN_FAST", "1")
+    if mode == "resident_idle_exits":
+        monkeypatch.setenv("MFX_DROPIN_IDLE_US", "20")
+    else:
+        monkeypatch.setenv("MFX_DROPIN_RESIDENT", "0")
+    ref = _random_scenario(common.ORACLE_LIB, 33, 60, 40, 3, 60, 50, episodes=2)
+    got = _random_scenario(common.HIP_LIB, 33, 60, 40, 3, 60, 50, episodes=2)
+    assert len(got) == len(ref)
+    first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
+    assert first_bad is None, "first divergence at step %s" % first_bad
+
+
+def test_dropin_two_resident_envs_interleaved(monkeypatch):
+    """Two drop-in envs in one process, stepped alternately: two resident servers on their own streams
+    at once, each answering only its own mailbox.  Each env's record stream equals the oracle's."""
+    monkeypatch.setenv("MFX_DROPIN_FAST", "1")
+
+    def run(lib, interleave):
+        envs = []
+        for k, (size, n) in enumerate([(24, 40), (40, 64)]):
+            env, h = common.battle_env(lib, size)
+            env.reset()
+            left, right = bd.block_positions(size, n)
+            env.add_agents(h[0], method="custom", pos=left)
+            env.add_agents(h[1], method="custom", pos=right)
+            _, v2a = env.get_view2attack(h[0])
+            envs.append([env, h, v2a, np.random.RandomState(10 + k), [], False])
+        order = [0, 1] * 40 if interleave else [0] * 40 + [1] * 40
+        for k in order:
+            env, h, v2a, rs, out, finished = envs[k]
+            if finished:
+                continue
+            obs = [env.get_observation(h[g]) for g in range(2)]
+            rec = [o[0].tobytes() + o[1].tobytes() for o in obs]
+            for g in range(2):
+                env.set_action(h[g], bd.rush_policy(obs[g][0], obs[g][1], rs, v2a, 13, 21, eps=0.3))
+            done = env.step()
+            for g in range(2):
+                rec.append(env.get_reward(h[g]).tobytes() + env.get_alive(h[g]).tobytes())
+            out.append(bd.sha(np.frombuffer(b"".join(rec) + bytes([done]), np.uint8)))
+            env.clear_dead()
+            envs[k][5] = done
+        return [e[4] for e in envs]
+
+    assert run(common.HIP_LIB, True) == run(common.ORACLE_LIB, False)
