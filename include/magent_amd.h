@@ -6,9 +6,11 @@
  * the reference python wrapper examples/battle_model/python/magent/gridworld.py (ctypes, no
  * argtypes) and c_lib.py:13-31 bind this library unchanged.  Those calls act on env 0 and move
  * data through caller-owned host buffers, exactly like the reference.  On one env whose config the
- * fused kernels take, set_action and clear_dead are deferred and env_step is ONE launch
- * (k_dropin_step) that also leaves the getters' records and the next observation in host-mapped
- * memory; any other call first runs the deferred work (MFX_DROPIN_FAST=0: one launch per call).
+ * fused kernels take, set_action and clear_dead are deferred and env_step is one request to a
+ * resident k_dropin_step workgroup (a mailbox in coherent host memory; MFX_DROPIN_RESIDENT=0: one
+ * launch per step) that also leaves the getters' record and the next observation in pinned memory;
+ * any other call first stops the server and runs the deferred work (MFX_DROPIN_FAST=0: one launch
+ * per call).
  *
  * Part 2 is this library's batched device API: E envs per engine, every buffer in HBM.
  * Part 3 covers the Ising lattice / tabular MF-Q (the reference's examples/ising_model and
@@ -81,10 +83,11 @@ int gridworld_define_event_node(void *game, int no, int op, int *inputs, int n_i
 int gridworld_add_reward_rule(void *game, int on, int *receiver, float *value, int n_receiver, bool is_terminal,
                               bool auto_value);
 /* Extension of env_get_observation (runtime_api.h:124) for the drop-in python: the same views and
- * features of env 0, as pointers into engine-owned pinned memory the drop-in step wrote them to (no
- * copy); valid until the step after next or env_delete_game.  Returns 1 (nothing set) when the
- * observation is not held that way -- call env_get_observation then. */
-int mfx_env_observation_view(void *game, int group, float **view, float **feature, int *n);
+ * features of env 0 (n agents), as pointers into engine-owned pinned memory the drop-in step wrote
+ * them to (no copy), in blocks of `rows` agents that stay at those addresses until the group
+ * outgrows them; valid until the step after next or env_delete_game.  Returns 1 (nothing set) when
+ * the observation is not held that way -- call env_get_observation then. */
+int mfx_env_observation_view(void *game, int group, float **view, float **feature, int *n, int *rows);
 
 /* ---------------------------------------------------------------- part 2: batched Battle */
 /* Before the first env_reset: make the engine hold n_envs identical envs. */

@@ -1618,7 +1618,7 @@ public:
     // the drop-in step into pinned memory (the set of the last request; the next request writes the
     // other set, so they stay valid until the step after next).  1: not available (the caller copies
     // through host_observe).
-    int observation_view(int g, float** view, float** feat, int* n) {
+    int observation_view(int g, float** view, float** feat, int* n, int* rows) {
         if (!allocated) return fail("get_observation before reset");
         if (g < 0 || g >= n_groups()) return fail("get_observation: bad group %d", g);
         MFX_CHECK(ensure_obs());
@@ -1628,6 +1628,7 @@ public:
         *view = reinterpret_cast<float*>(pin_fast.p + o + fast_view[g]);
         *feat = reinterpret_cast<float*>(pin_fast.p + o + fast_feat[g]);
         *n = hn[g];
+        *rows = (int)fast_rows;
         return 0;
     }
     // No sync: the actions go out of pinned memory (one region per group, reused once the previous
@@ -1962,10 +1963,10 @@ MFX_API int env_config_game(void* game, const char* name, void* value) { MFX_GUA
 MFX_API int env_reset(void* game) { MFX_GUARD(MFX_ENV(game)->reset()); }
 MFX_API int env_get_observation(void* game, int group, float** buffer) { MFX_GUARD(MFX_ENV(game)->host_observe(group, buffer)); }
 // get_observation without the copy (the drop-in fast step): pointers to env 0's observation of the
-// group in engine-owned pinned memory, valid until the step after next or the engine's deletion.
-// Returns 1 when the observation is not held that way (use env_get_observation).
-MFX_API int mfx_env_observation_view(void* game, int group, float** view, float** feature, int* n) {
-    MFX_GUARD(MFX_ENV(game)->observation_view(group, view, feature, n));
+// group in engine-owned pinned memory (n rows of blocks of `rows`), valid until the step after next or
+// the engine's deletion.  Returns 1 when the observation is not held that way (use env_get_observation).
+MFX_API int mfx_env_observation_view(void* game, int group, float** view, float** feature, int* n, int* rows) {
+    MFX_GUARD(MFX_ENV(game)->observation_view(group, view, feature, n, rows));
 }
 MFX_API int env_set_action(void* game, int group, const int* actions) { MFX_GUARD(MFX_ENV(game)->host_set_action(group, actions)); }
 MFX_API int env_step(void* game, int* done) { MFX_GUARD(MFX_ENV(game)->host_step(done)); }

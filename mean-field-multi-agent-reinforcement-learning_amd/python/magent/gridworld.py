@@ -22,6 +22,20 @@ _CONFIG_TYPES = {
 }
 
 
+class _Engine:
+    """Owner of one engine handle: env_delete_game runs when the GridWorld and every observation view
+    handed out by get_observation (which point into the engine's pinned memory) are gone."""
+    __slots__ = ("lib", "game")
+
+    def __init__(self, lib, game):
+        self.lib, self.game = lib, game
+
+    def __del__(self):
+        if self.game is not None and self.game.value:
+            self.lib.dll.env_delete_game(self.game)
+            self.game = None
+
+
 class GridWorld(Environment):
     OBS_INDEX_VIEW = 0
     OBS_INDEX_HP = 1
@@ -42,6 +56,7 @@ class GridWorld(Environment):
         game = ctypes.c_void_p()
         L.env_new_game(ctypes.byref(game), b"GridWorld")
         self.game = game
+        self._engine = _Engine(L, game)      # deletes the engine once neither this env nor a view needs it
 
         for key, value in config.config_dict.items():
             kind = _CONFIG_TYPES[key]
@@ -78,9 +93,13 @@ class GridWorld(Environment):
         # engines that hold the drop-in step's observation in pinned memory hand it out without a copy
         self._obs_view = getattr(L.dll, "mfx_env_observation_view", None) if hasattr(L, "dll") else None
         if self._obs_view is not None:
-            fp = ctypes.POINTER(ctypes.POINTER(ctypes.c_float))
-            self._obs_view.argtypes = [ctypes.c_void_p, ctypes.c_int, fp, fp, ctypes.POINTER(ctypes.c_int32)]
+            vp = ctypes.POINTER(ctypes.c_void_p)
+            ip = ctypes.POINTER(ctypes.c_int32)
+            self._obs_view.argtypes = [ctypes.c_void_p, ctypes.c_int, vp, vp, ip, ip]
             self._obs_view.restype = ctypes.c_int
+            self._ov_out = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32(), ctypes.c_int32())
+            self._ov_ref = tuple(ctypes.byref(x) for x in self._ov_out)
+            self._ov_blocks = {}                 # (address, rows, shape) -> array over that pinned block
         self.view_space, self.feature_space, self.action_space = {}, {}, {}
         buf = np.empty((3,), dtype=np.int32)
         for h in self.group_handles:
@@ -143,16 +162,19 @@ class GridWorld(Environment):
             ret = bufs[group] = np.empty(shape=shape, dtype=dtype)
         return ret
 
-    def _pinned(self, ptr, shape):
-        """float32 array over engine-owned memory; it keeps this env (and so the memory) alive."""
-        count = 1
-        for d in shape:
-            count *= d
-        if count == 0:
-            return np.empty(shape, dtype=np.float32)
-        buf = (ctypes.c_float * count).from_address(ctypes.addressof(ptr.contents))
-        buf._owner = self
-        return np.frombuffer(buf, dtype=np.float32).reshape(shape)
+    def _block(self, addr, rows, space):
+        """float32 [rows, *space] array over the engine-owned pinned block at addr (made once per block);
+        it keeps the engine (self._engine), not this env, alive."""
+        key = (addr, rows, space)
+        b = self._ov_blocks.get(key)
+        if b is None:
+            count = rows
+            for d in space:
+                count *= d
+            buf = (ctypes.c_float * count).from_address(addr)
+            buf._owner = self._engine
+            b = self._ov_blocks[key] = np.frombuffer(buf, dtype=np.float32).reshape((rows,) + space)
+        return b
 
     def get_observation(self, handle):
         """(views [n, H, W, C] float32, features [n, F] float32) of every agent of the group.
@@ -162,11 +184,13 @@ class GridWorld(Environment):
         step after next, which leaves them valid through the replay push that follows env.step()."""
         g = _hv(handle)
         if self._obs_view is not None:
-            vp, fp, n = ctypes.POINTER(ctypes.c_float)(), ctypes.POINTER(ctypes.c_float)(), ctypes.c_int32()
-            r = self._obs_view(self.game, g, ctypes.byref(vp), ctypes.byref(fp), ctypes.byref(n))
+            ref = self._ov_ref
+            r = self._obs_view(self.game, g, ref[0], ref[1], ref[2], ref[3])
             if r == 0:
-                n = n.value
-                return self._pinned(vp, (n,) + self.view_space[g]), self._pinned(fp, (n,) + self.feature_space[g])
+                vp, fp, n, rows = self._ov_out
+                n, rows = n.value, rows.value
+                return (self._block(vp.value, rows, self.view_space[g])[:n],
+                        self._block(fp.value, rows, self.feature_space[g])[:n])
             if r < 0:
                 raise EngineError("mfx_env_observation_view failed (%d): %s"
                                   % (r, self._lib.dll.mfx_last_error().decode()))
@@ -287,11 +311,7 @@ class GridWorld(Environment):
         self._lib.env_render(self.game)
 
     def __del__(self):
-        game = getattr(self, "game", None)
-        lib = getattr(self, "_lib", None)
-        if game is not None and lib is not None and game.value:
-            lib.dll.env_delete_game(game)
-            self.game = ctypes.c_void_p()
+        self._engine = None                  # the engine goes when the last observation view does
 
     # ------------------------------------------------------------------ reward description
     def _serialize_event_exp(self, config):
