@@ -181,6 +181,14 @@ public:
     bool fast_res = false;                   // the last request went to the resident server
     int res_relaunch = 0;                    // relaunches after an idle exit (statistics)
     MappedBuf<DropinMailbox> mbox;
+    uint32_t mail_tag[kMaxGroups] = {};      // tag of group g's actions in mbox->acts (~0: not there)
+    size_t mail_stride[kMaxGroups] = {};     //   and the per-group stride they were written with
+    int ensure_mbox() {
+        if (mbox.p) return 0;
+        try { mbox.ensure(1, hipHostMallocCoherent); } catch (const HipFailure& f) { return fail("%s", f.what()); }
+        memset(mbox.p, 0, sizeof(DropinMailbox));
+        return 0;
+    }
     DropinArgs res_da{};                     // the arguments of the live server (relaunch)
     static bool env_flag(const char* name, bool dflt) {
         const char* v = getenv(name);
@@ -1372,6 +1380,22 @@ public:
             return fail("%s", f.what());
         }
         if (n) memcpy(pin_fact.p + (size_t)g * fact_rows, actions, sizeof(int) * n);
+        // the resident server also finds them in its mailbox, tagged with the request that will carry
+        // them (read in the same poll as the request, battle/dropin.inc dropin_wait)
+        mail_tag[g] = ~0u;
+        if (res_enabled && own_stream && env_flag("MFX_DROPIN_MAIL", false) &&
+            (size_t)n_groups() * fact_rows <= (size_t)kMailActs) {
+            bool ok = true;
+            for (int i = 0; i < n && ok; i++) ok = (uint32_t)actions[i] <= 0xFFFFu;
+            if (ok) {
+                if (ensure_mbox() != 0) return -1;
+                const uint32_t tag = (fast_seq + 1) & 0xFFFFu;
+                uint32_t* d = mbox.p->acts + (size_t)g * fact_rows;
+                for (int i = 0; i < n; i++) d[i] = (tag << 16) | (uint32_t)actions[i];
+                mail_tag[g] = tag;
+                mail_stride[g] = fact_rows;
+            }
+        }
         acts_since_step[g]++;
         defer_act[g] = true;
         defer_n[g] = n;
@@ -1447,21 +1471,28 @@ public:
         begin_step();
         fast_res = res_enabled && own_stream && !s.serial_step;
         if (fast_res) {
-            if (!mbox.p) {
-                try { mbox.ensure(1, hipHostMallocCoherent); } catch (const HipFailure& f) { return fail("%s", f.what()); }
-                memset(mbox.p, 0, sizeof(DropinMailbox));
-            }
+            MFX_CHECK(ensure_mbox());
             DropinMailbox* mb = mbox.p;
+            const uint32_t seq = ++fast_seq;
+            bool tagged = true;
+            for (int g = 0; g < G; g++)
+                if (defer_act[g] && (mail_tag[g] != (seq & 0xFFFFu) || mail_stride[g] != fact_rows)) tagged = false;
             mb->cmd = kDropinStep;
             mb->pending_clear = defer_clear;
             for (int g = 0; g < kMaxGroups; g++) mb->n_acts[g] = g < G && defer_act[g] ? defer_n[g] : -1;
-            const uint32_t seq = ++fast_seq;
+            mb->tagged = tagged;
+            mb->act_stride = (int32_t)std::max<size_t>(fact_rows, 1);
             __atomic_store_n(&mb->req, seq, __ATOMIC_RELEASE);
             if (!res_live) {
                 for (int g = 0; g < G; g++) da.acts[g] = pin_fact.d + (size_t)g * fact_rows;
                 da.mb = mbox.d;
                 da.seq = seq - 1;
                 da.idle = res_idle_ticks();
+                {   // MFX_DROPIN_MAIL=1: poll the tagged actions with the header (just the words they need)
+                    const size_t words = 16 + (size_t)G * fact_rows;
+                    da.mail_passes = words <= 256 ? 1 : words <= (size_t)kMailWords ? 2 : 0;
+                    if (!env_flag("MFX_DROPIN_MAIL", false)) da.mail_passes = 0;   // measured neutral: off
+                }
                 da.variant = res_variant();
                 res_da = da;
                 MFX_HIP(launch_dropin_step(gp, d_gp, s, da, stream));

@@ -146,12 +146,17 @@ struct State {                      // device pointers; every array is [E][strid
 // memory.  The host writes a request's fields, then `req` (release); the kernel answers in `done`,
 // on its own 128-B line so that the two sides do not write one line.
 enum : int32_t { kDropinStop = 0, kDropinStep = 1 };
+// the request line and the tagged actions: one 16-B load per lane of wave 0, two passes (512 words)
+constexpr int kMailWords = 512, kMailActs = kMailWords - 16;
 struct DropinMailbox {
-    uint32_t req;                        // sequence number of the latest request
-    int32_t cmd;                         // kDropinStep / kDropinStop
-    int32_t pending_clear;               // a clear_dead is deferred from the previous step
-    int32_t n_acts[kMaxGroups];          // deferred set_action lengths, -1: no call for the group
-    int32_t pad0[32 - 3 - kMaxGroups];
+    uint32_t req;                        // word 0: sequence number of the latest request
+    int32_t cmd;                         // 1: kDropinStep / kDropinStop
+    int32_t pending_clear;               // 2: a clear_dead is deferred from the previous step
+    int32_t n_acts[kMaxGroups];          // 3-6: deferred set_action lengths, -1: no call for the group
+    int32_t tagged;                      // 7: the actions are in acts[], each word (req & 0xFFFF) << 16 | action
+    int32_t act_stride;                  // 8: words per group in acts[]
+    int32_t pad0[7];
+    uint32_t acts[kMailActs];            // words 16..511: group g's actions from g * act_stride
     uint32_t done[4];                    // [0] records written, [1] observation written, [2] unused,
                                          // [3] the kernel has left (the last request it saw)
     int32_t pad1[28];
@@ -174,6 +179,8 @@ struct DropinArgs {
     // request already answered; flag is unused.
     DropinMailbox* mb;
     unsigned long long idle;
+    int mail_passes;                     // 16-B loads per lane and poll: 1 or 2 (header + tagged actions,
+                                         // 256 / 512 words), 0: the header only (actions read after)
     int variant;                         // diagnostics (MFX_DROPIN_VARIANT): bit 1 answers requests
                                          // without doing the step (timing only),
                                          // bit 3 writes the record in system-scope stores and publishes
