@@ -43,7 +43,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 24576 at 64x64, 1024 at 256x256)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 49152 at 64x64, 1024 at 256x256)")
     ap.add_argument("--total-envs", type=int, default=None,
                     help="envs over all GPUs, split evenly (strong scaling; configs[3]: --total-envs 64)")
     ap.add_argument("--map", type=int, default=MAP, help="map side (64: the metric's config; 256: configs[4])")
@@ -65,10 +65,10 @@ def parse(argv=None):
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     if a.envs is None and a.total_envs is None:
-        # 64x64: 24576 envs per GPU -- a launch has a fixed cost (~0.15 ms: ramp-up and the tail of the
-        # persistent grid), amortised over more envs: 16384 -> 24576 envs = +6-11 % agent-steps/s,
-        # beyond ~28K the gain stops (profiles/r01_env_sweep.txt)
-        a.envs = 24576 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
+        # 64x64: 49152 envs per GPU (~60 GB of observation buffers) -- a launch has a fixed cost (ramp-up
+        # and the tail of the persistent grid), amortised over more envs: at 4 steps per launch 24576 ->
+        # 32768 -> 49152 envs = 1.09 -> 1.137 -> 1.146e9 agent-steps/s (profiles/r02_env_sub_sweep.txt)
+        a.envs = 49152 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
     return a
 
 

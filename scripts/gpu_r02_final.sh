@@ -3,7 +3,7 @@
 # FETCH_SIZE / WRITE_SIZE passes for both (one counter block per pass).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r02f
+O=gpurun_out/r02g
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
