@@ -247,17 +247,20 @@ def test_dropin_odd_call_orders(seed, fast, monkeypatch):
     assert first_bad is None, "first divergence at record %s" % first_bad
 
 
-@pytest.mark.parametrize("mode", ["resident_idle_exits", "one_launch_per_step"])
+@pytest.mark.parametrize("mode", ["resident_idle_exits", "one_launch_per_step", "actions_in_mailbox_poll"])
 def test_dropin_resident_server_modes(mode, monkeypatch):
     """The resident drop-in server (one k_dropin_step launch answering env.step() through a mailbox)
     with an idle timeout of 20 us, so that it leaves between nearly every pair of steps and is
-    relaunched with the request already posted (the relaunch race); and the one-launch-per-step form
-    (MFX_DROPIN_RESIDENT=0).  Both against the C oracle, two episodes with walls and random placement."""
+    relaunched with the request already posted (the relaunch race); the one-launch-per-step form
+    (MFX_DROPIN_RESIDENT=0); and the tagged actions read inside the request poll (MFX_DROPIN_MAIL=1).
+    All against the C oracle, two episodes with walls and random placement."""
     monkeypatch.setenv("MFX_DROPIN_FAST", "1")
     if mode == "resident_idle_exits":
         monkeypatch.setenv("MFX_DROPIN_IDLE_US", "20")
-    else:
+    elif mode == "one_launch_per_step":
         monkeypatch.setenv("MFX_DROPIN_RESIDENT", "0")
+    else:
+        monkeypatch.setenv("MFX_DROPIN_MAIL", "1")
     ref = _random_scenario(common.ORACLE_LIB, 33, 60, 40, 3, 60, 50, episodes=2)
     got = _random_scenario(common.HIP_LIB, 33, 60, 40, 3, 60, 50, episodes=2)
     assert len(got) == len(ref)

@@ -359,6 +359,72 @@ def test_rollout_bench_shape_matches_oracle():
     assert restarts >= len(sample)
 
 
+def test_rollout_large_env_staggered_many_envs_matches_oracle():
+    """The large-env pipeline with more envs than XCD item lists: 16 staggered 200x200 envs (1250 per
+    side) in two sub-batch pipelines, so each of the 8 per-XCD observation item lists holds an env
+    of each sub-batch and the workgroups of every XCD help the others' lists; 32 steps with an
+    episode cap of 24 (every env restarts).  Every env replayed on the C oracle: views, features,
+    rewards, mean actions, bit for bit."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, T, max_steps, VF, F, M = 16, 32, 24, 13 * 13 * 7, 34, 200
+    left, right = bd.block_positions(M, 1250)
+    eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=99, stagger=True)
+    grid, lds = eng.rollout_info()
+    assert lds > 64 * 1024                           # the large-env path
+    rc = eng.rowcap
+    envs = []
+    for e in range(E):
+        env, h = common.battle_env(common.ORACLE_LIB, M)
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        envs.append([env, h, e * max_steps // E])
+    restarts = 0
+    for t in range(T):
+        eng.rollout_step(1)
+        view = [torch.empty(E * rc * VF, dtype=torch.float32) for _ in range(2)]
+        feat = [torch.empty(E * rc * F, dtype=torch.float32) for _ in range(2)]
+        act = torch.empty(E * 2 * rc, dtype=torch.int32)
+        rew = torch.empty(E * 2 * rc, dtype=torch.float32)
+        mean = torch.empty(E * 2 * 21, dtype=torch.float64)
+        for g in range(2):
+            eng.rollout_copy("view", view[g], group=g)
+            eng.rollout_copy("feature", feat[g], group=g)
+        eng.rollout_copy("actions", act)
+        eng.rollout_copy("rewards", rew)
+        eng.rollout_copy("mean_action", mean)
+        eng.sync()
+        for e, st in enumerate(envs):
+            env, h, _ = st
+            acts = []
+            for g in range(2):
+                v, f = env.get_observation(h[g])
+                n = len(v)
+                assert view[g].numpy().reshape(E, rc, VF)[e, :n].tobytes() == v.reshape(n, VF).tobytes(), (e, t, g)
+                assert feat[g].numpy().reshape(E, rc, F)[e, :n].tobytes() == f.tobytes(), (e, t, g)
+                a = act.numpy().reshape(E, 2, rc)[e, g, :n].astype(np.int32)
+                acts.append(a)
+                m = np.bincount(a, minlength=21) / n if n else np.full(21, np.nan)
+                assert np.array_equal(mean.numpy().reshape(E, 2, 21)[e, g], m, equal_nan=True), (e, t, g)
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rw = env.get_reward(h[g])
+                assert rew.numpy().reshape(E, 2, rc)[e, g, :len(rw)].tobytes() == rw.tobytes(), (e, t, g, "reward")
+            env.clear_dead()
+            st[2] += 1
+            if done or st[2] >= max_steps:
+                st[2] = 0
+                restarts += 1
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
+    assert restarts >= E
+
+
 @pytest.mark.parametrize("sub", [2, 7])
 def test_rollout_substeps_match_single_steps(sub):
     """k_rollout running `sub` consecutive steps of each env per launch (image kept in LDS) leaves
