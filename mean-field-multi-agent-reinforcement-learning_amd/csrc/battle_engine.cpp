@@ -1482,6 +1482,9 @@ public:
             for (int g = 0; g < kMaxGroups; g++) mb->n_acts[g] = g < G && defer_act[g] ? defer_n[g] : -1;
             mb->tagged = tagged;
             mb->act_stride = (int32_t)std::max<size_t>(fact_rows, 1);
+            // a server that left on its idle timeout wrote the last request it answered into done[3]
+            // on its way out: relaunch it at once (wait_fast's stream query would notice ~100 us later)
+            if (res_live && __atomic_load_n(&mb->done[3], __ATOMIC_ACQUIRE) == seq - 1) res_live = false;
             __atomic_store_n(&mb->req, seq, __ATOMIC_RELEASE);
             if (!res_live) {
                 for (int g = 0; g < G; g++) da.acts[g] = pin_fact.d + (size_t)g * fact_rows;
@@ -1568,14 +1571,16 @@ public:
         static const int v = getenv("MFX_DROPIN_VARIANT") ? atoi(getenv("MFX_DROPIN_VARIANT")) : 0;
         return v;
     }
+    static long long res_idle_us() {                       // (read each time: tests change it)
+        const char* v = getenv("MFX_DROPIN_IDLE_US");
+        return v ? std::max(1, atoi(v)) : 2000;
+    }
     unsigned long long res_idle_ticks() const {
         int dev = 0, khz = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
             khz <= 0)
             khz = 100000;                                  // gfx9: 100 MHz
-        const char* v = getenv("MFX_DROPIN_IDLE_US");
-        const long long us = v ? std::max(1, atoi(v)) : 2000;
-        return (unsigned long long)us * (unsigned long long)khz / 1000ull;
+        return (unsigned long long)res_idle_us() * (unsigned long long)khz / 1000ull;
     }
     // clear_dead right after a fast step: deferred; the step's launch already left what the getters
     // and get_observation ask next.

@@ -23,6 +23,7 @@ ap.add_argument("--map", type=int, default=64)
 ap.add_argument("--agents", type=int, default=256)
 ap.add_argument("--seconds", type=float, default=5.0)
 ap.add_argument("--calls", action="store_true", help="also report the time per call kind (us per step)")
+ap.add_argument("--pause-us", type=float, default=0.0, help="host pause per step outside the clock (a slow policy)")
 a = ap.parse_args()
 
 
@@ -58,6 +59,10 @@ def run(lib_path, per_call=None):
                 ck.t("get_agent_id", env.get_agent_id, h[g])
             clock += time.perf_counter() - t
             acts = [bd.rush_policy(obs[g][0], obs[g][1], rng, v2a, 13, 21) for g in range(2)]
+            if a.pause_us:
+                t_end = time.perf_counter() + a.pause_us * 1e-6
+                while time.perf_counter() < t_end:
+                    pass
             t = time.perf_counter()
             for g in range(2):
                 ck.t("set_action", env.set_action, h[g], acts[g])
