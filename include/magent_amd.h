@@ -111,8 +111,9 @@ int mfx_battle_group_capacity(void *game, int group, int *cap);
 int mfx_battle_rollout_init(void *game, const int *tmpl_n, const int *const *xs, const int *const *ys,
                             int max_steps, float eps, unsigned seed, int stagger);
 int mfx_battle_rollout_step(void *game, int n_steps);
-/* Steps per k_rollout launch (1..64, default 1): each env runs that many consecutive steps with its
- * image resident in LDS.  rollout_step(n) gives identical results for every value. */
+/* Steps per launch (1..64, default 1): k_rollout runs each env's steps back to back with its image
+ * resident in LDS; the large-env queue kernel (k_rollout_bigq) runs every env's steps in one launch.
+ * rollout_step(n) gives identical results for every value. */
 int mfx_battle_rollout_set_substeps(void *game, int n_sub);
 /* names: view, feature, actions, rewards, mean_action, episode_return, stats, agent_steps, group_num */
 int mfx_battle_rollout_buffer(void *game, const char *name, int group, void **d_ptr, size_t *bytes);
@@ -122,6 +123,9 @@ int mfx_battle_rollout_copy_at(void *game, const char *name, int group, size_t o
 int mfx_battle_rollout_rowcap(void *game, int *rowcap);
 /* Persistent grid (workgroups per launch) and dynamic LDS bytes per workgroup of the fused rollout. */
 int mfx_battle_rollout_info(void *game, int *grid, int *lds_bytes);
+/* Large envs: -1 (message in mfx_last_error) if the in-launch work queue of k_rollout_bigq ever
+ * stalled; synchronises the engine stream. */
+int mfx_battle_rollout_check(void *game);
 /* Diagnostic build only (libmagent_stamps.so): per-phase s_memtime stamps [E][16]. */
 int mfx_battle_set_stamp_buffer(void *d_buf);
 

@@ -211,6 +211,14 @@ public:
     DevBuf<uint32_t> ro_items;               //             observation work items        [2][E*G*slots]
     DevBuf<int32_t> ro_cnt;                  //             their counters                [split][2][2]
     int ro_item_grid = 0;                    //             persistent grid of k_observe_items
+    // large envs, queue-driven (k_rollout_bigq, default): one launch per ro_sub steps of every env
+    bool ro_bigq = false;
+    bool ro_bigq_want = true;                // MFX_BIG_FUSED=0 at rollout_init: the two-stream pipeline (A/B)
+    DevBuf<uint32_t> ro_q_items, ro_q_si;    // [2][kXcds][list cap] tagged items; [E] next step index
+    DevBuf<int32_t> ro_q_cnt, ro_q_left, ro_q_done;
+    int ro_q_grid = 0, ro_qpar = 0;
+    uint32_t ro_qlaunch = 0, ro_qdone = 0;   // launches so far (item tags); env-steps the queue has done
+    static uint32_t qtag(uint32_t launch) { return launch % 4095u + 1u; }
     bool ro_prep_stale = true;               // ro_mm / ro_info / items lag the state (per-call calls since)
     DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
     DevBuf<double> ro_mean, ro_stats;
@@ -234,6 +242,7 @@ public:
     // k_observe_items slots, leaving room for the other stream's step.  Measured at 256x256 / 4096
     // agents, 1024 envs (profiles/r01_big_sweeps.txt): 2 streams / 1/3 grid / 64-agent items best.
     static constexpr int kBigSplit = 2, kItemGridDiv = 3, kItemRows = 64;
+    static constexpr int kBigqRows = 64;          // agents per k_rollout_bigq observation item
     static constexpr bool kPipeDefault = false;   // measured slower than the fused step
     static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
@@ -1059,6 +1068,10 @@ public:
             if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return fail("rollout: 1x1 bodies only; use the per-call API");
         try {
             ensure_capacity(total, total);
+            {
+                const char* fv = getenv("MFX_BIG_FUSED");
+                ro_bigq_want = !(fv && atoi(fv) == 0);
+            }
             const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rowcap);
             // envs too large for one workgroup's LDS run k_observe + k_rollout_big with the state in HBM
             ro_big = smem > 160 * 1024;
@@ -1159,6 +1172,32 @@ public:
                     const char* gd = getenv("MFX_ITEM_GRID_DIV");   // sweeps only
                     ro_item_grid = std::max(1, ro_item_grid / (gd ? std::max(1, atoi(gd)) : kItemGridDiv));
                     if (ro_item_grid >= kXcds) ro_item_grid -= ro_item_grid % kXcds;   // as many per XCD
+                    // the queue-driven kernel: item words hold 13 env bits and 6 chunk bits
+                    const char* rv = getenv("MFX_BIGQ_ROWS");                  // sweeps only
+                    const int Rq = rv && atoi(rv) > 0 ? atoi(rv) : kBigqRows;
+                    const int chunks = (ra.rowcap + Rq - 1) / Rq;
+                    ro_bigq = ro_bigq_want && E <= 8192 && chunks <= 64 && n_groups() == 2 &&
+                              bigq_smem_bytes(gp, s.cap, s.acap, Rq) <= 160 * 1024;
+                    if (ro_bigq) MFX_HIP_THROW(bigq_grid(gp, s.cap, s.acap, Rq, &ro_q_grid));
+                    ro_bigq = ro_bigq && ro_q_grid > 0;          // (0: not one SPX device of 8 XCDs)
+                    if (ro_bigq) {
+                        // per list and parity: one filing per env and step of a launch (<= 64 steps)
+                        // (+ the tickets idle workgroups hold past the last filing: one per workgroup)
+                        const size_t lcap = (size_t)((E + kXcds - 1) / kXcds) * 64 * (size_t)(n_groups() * chunks) +
+                                            (size_t)ro_q_grid;
+                        ro_q_items.ensure(2 * kXcds * lcap);
+                        ro_q_cnt.ensure(2 * kXcds * kObsCntPad);
+                        ro_q_left.ensure(E); ro_q_si.ensure(E); ro_q_done.ensure(kObsCntPad);
+                        MFX_HIP_THROW(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
+                        MFX_HIP_THROW(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
+                        ra.q_items = ro_q_items.p; ra.q_cnt = ro_q_cnt.p; ra.q_left = ro_q_left.p;
+                        ra.q_si = ro_q_si.p; ra.q_done = ro_q_done.p; ra.q_list_cap = lcap;
+                        ra.obs_item_rows = Rq;
+                        const char* qg = getenv("MFX_BIGQ_GRID");               // sweeps only
+                        if (qg && atoi(qg) > 0) ro_q_grid = std::min(ro_q_grid, atoi(qg));
+                    }
+                } else {
+                    ro_bigq = false;
                 }
                 const int K = std::min(ro_split, E);
                 ro_sub_ctx.ensure(K);
@@ -1214,6 +1253,32 @@ public:
         {
             const State& planned = ro_pipe ? ro_pipe_host[ro_par].s : ro_ctx_host.s;
             if (s.cap != ro_cap || memcmp(&planned, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
+        }
+        if (ro_big && ro_bigq) {
+            MFX_CHECK(sync_cells());
+            const size_t lst = (size_t)kXcds * kObsCntPad;           // counters of one parity
+            if (ro_prep_stale) {
+                ro_qpar = 0;
+                ro_qdone = 0;
+                MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, 2 * lst * sizeof(int32_t), stream));
+                MFX_HIP(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
+                MFX_HIP(launch_bigq_seed(d_gp, s, ra, ro_qpar, qtag(ro_qlaunch), ra.step_index, stream));
+            }
+            ro_prep_stale = false;
+            for (int i = 0; i < n_steps;) {
+                const int k = std::min(ro_sub, n_steps - i);
+                MFX_HIP(hipMemsetAsync(ro_q_cnt.p + (ro_qpar ^ 1) * lst, 0, lst * sizeof(int32_t), stream));
+                ro_qdone += (uint32_t)E * (uint32_t)k;
+                MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, ro_qpar,
+                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
+                                            stream));
+                ro_qpar ^= 1;
+                ro_qlaunch++;
+                ro_launch++;
+                ra.step_index += k;
+                i += k;
+            }
+            return 0;
         }
         if (ro_big) {
             MFX_CHECK(sync_cells());
@@ -1280,6 +1345,17 @@ public:
             cells_stale = true;
             i += k;
         }
+        return 0;
+    }
+
+    // The queue-driven large-env kernel's error word (a queue that stopped making progress): 0 if none.
+    int rollout_check() {
+        if (!rollout_ready) return fail("rollout_check before rollout_init");
+        if (!(ro_big && ro_bigq)) return 0;
+        int32_t w[kObsCntPad] = {};
+        MFX_HIP(hipMemcpyAsync(w, ro_q_done.p, sizeof(w), hipMemcpyDeviceToHost, stream));
+        MFX_HIP(hipStreamSynchronize(stream));
+        if (w[2]) return fail("rollout: the large-env work queue stalled (code %d)", w[2]);
         return 0;
     }
 
@@ -2133,6 +2209,11 @@ MFX_API int mfx_battle_set_stamp_buffer(void* d_buf) {
 // Launch geometry of the fused rollout: persistent grid (workgroups) and LDS bytes per workgroup.
 MFX_API int mfx_battle_rollout_info(void* game, int* grid, int* lds_bytes) {
     MFX_GUARD(MFX_ENV(game)->rollout_info(grid, lds_bytes));
+}
+
+// Large envs (k_rollout_bigq): -1 and the message if the in-launch work queue ever stalled (syncs).
+MFX_API int mfx_battle_rollout_check(void* game) {
+    MFX_GUARD(MFX_ENV(game)->rollout_check());
 }
 
 // Steps per k_rollout launch (1..64): every env runs that many consecutive steps while its image stays

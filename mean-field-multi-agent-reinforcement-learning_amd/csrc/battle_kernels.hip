@@ -285,6 +285,41 @@ hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, cons
     return hipGetLastError();
 }
 
+size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows) {
+    const size_t a = big_step_smem_bytes(gp, cap, acap, true);
+    const size_t b = obs_smem_core(gp, 0, 0, rows, obs_stage_floats(gp, 0, true, kBigRolloutThreads), true);
+    return a > b ? a : b;
+}
+
+hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, int* grid) {
+    const size_t smem = bigq_smem_bytes(gp, cap, acap, rows);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (err == hipSuccess)
+        err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rollout_bigq, kBigRolloutThreads, smem);
+    if (err != hipSuccess) return err;
+    // one device of 8 XCDs (SPX): every XCD gets workgroups of the full-occupancy grid (k_rollout_bigq)
+    *grid = (cus % kXcds == 0 && cus >= 8 * kXcds) ? cus * (per_cu > 0 ? per_cu : 1) : 0;
+    return hipSuccess;
+}
+
+hipError_t launch_bigq_seed(const GameParams* d_gp, const State& s, const RolloutArgs& ra, int par, uint32_t tag,
+                            uint32_t step_index, hipStream_t st) {
+    k_bigq_seed<<<s.E, 256, 0, st>>>(d_gp, s, ra, par, tag, step_index);
+    return hipGetLastError();
+}
+
+hipError_t launch_rollout_bigq(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                               int rows, uint32_t si0, int n_sub, int par, uint32_t tag_cur, uint32_t tag_next,
+                               int32_t done_target, int grid, hipStream_t st) {
+    const size_t smem = bigq_smem_bytes(gp, s.cap, s.acap, rows);
+    if (smem > 160 * 1024 || grid < 1 || n_sub < 1) return hipErrorInvalidValue;
+    k_rollout_bigq<<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
+                                                          done_target);
+    return hipGetLastError();
+}
+
 hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st) {
     k_clear_dead<<<s.E, 256, 0, st>>>(d_gp, s);
     return hipGetLastError();

@@ -233,6 +233,12 @@ struct RolloutArgs {
     size_t obs_list_stride;         //   items per list
     int obs_lists;                  //   1 or kXcds
     int obs_item_rows;              //   agents per item
+    uint32_t* q_items;              // large envs, k_rollout_bigq: [2][kXcds][q_list_cap] tagged work items
+    int32_t* q_cnt;                 //   [2][kXcds][kObsCntPad] items filed, items taken
+    int32_t* q_left;                //   [E] items of the env's current step not yet observed
+    uint32_t* q_si;                 //   [E] the env's next step index
+    int32_t* q_done;                //   [kObsCntPad] 0: env-steps done (monotone), 2: stuck-queue error word
+    size_t q_list_cap;              //   items per list and parity
     const uint4* wall_image;        // [H*W] u16 cells of that image with the agents removed: every
                                     // install rebuilds the cells from it plus the agents' positions, so
                                     // per-env cells are neither read nor written back (State::cells is

@@ -32,7 +32,7 @@ class BattleBatch:
                    "mfx_battle_sync", "mfx_battle_rollout_init", "mfx_battle_rollout_step",
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
-                   "mfx_battle_rollout_copy_at"):
+                   "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check"):
             try:
                 getattr(self._dll, fn).restype = ctypes.c_int
             except AttributeError:          # an older build of the library (A/B runs)
@@ -114,6 +114,10 @@ class BattleBatch:
         g, b = ctypes.c_int(), ctypes.c_int()
         self._check(self._dll.mfx_battle_rollout_info(self.game, ctypes.byref(g), ctypes.byref(b)), "rollout_info")
         return g.value, b.value
+
+    def rollout_check(self):
+        """Raise if the large-env queue kernel (k_rollout_bigq) ever stalled (synchronises)."""
+        self._check(self._dll.mfx_battle_rollout_check(self.game), "rollout_check")
 
     def rollout_substeps(self, n_sub):
         """Consecutive steps of every env per k_rollout launch (results do not depend on it)."""

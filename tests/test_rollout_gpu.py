@@ -167,6 +167,7 @@ def test_rollout_large_env_matches_oracle(map_size, n_side, E, T, max_steps):
                 env.reset()
                 env.add_agents(h[0], method="custom", pos=left)
                 env.add_agents(h[1], method="custom", pos=right)
+    eng.rollout_check()                           # the queue kernel never stalled
     assert kills > 0                              # the attack fixed point saw real kills
 
 
@@ -422,7 +423,65 @@ def test_rollout_large_env_staggered_many_envs_matches_oracle():
                 env.reset()
                 env.add_agents(h[0], method="custom", pos=left)
                 env.add_agents(h[1], method="custom", pos=right)
+    eng.rollout_check()
     assert restarts >= E
+
+
+def test_rollout_large_env_queue_matches_pipeline(monkeypatch):
+    """The queue-driven large-env kernel (k_rollout_bigq: observation items and the steps they gate in
+    one launch, several steps of every env per launch, items filed inside the launch) against the
+    two-stream pipeline (k_observe_items + k_rollout_big, checked on the oracle above): 24 staggered
+    200x200 envs, episode cap 24 (restarts inside launches), 1 and 5 steps per launch; every output
+    buffer bit for bit after 13 and 43 steps, and no stalled queue."""
+    import ctypes
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, M = 24, 200
+    left, right = bd.block_positions(M, 1250)
+    engs = []
+    for fused, sub in (("0", 1), ("1", 1), ("1", 5)):
+        monkeypatch.setenv("MFX_BIG_FUSED", fused)
+        eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=24, eps=0.3, seed=41, stagger=True)
+        eng.rollout_substeps(sub)
+        engs.append(eng)
+
+    N = 1250                 # rows every env wrote at its first step (the rows past them were never written)
+
+    def dump(eng):
+        out, rc = [], eng.rowcap
+        for name, dt in (("actions", torch.int32), ("rewards", torch.float32), ("mean_action", torch.float64),
+                         ("stats", torch.float64), ("agent_steps", torch.int64), ("group_num", torch.int32),
+                         ("episode_return", torch.float32)):
+            ptr, nb = ctypes.c_void_p(), ctypes.c_size_t()
+            eng._dll.mfx_battle_rollout_buffer(eng.game, name.encode(), 0, ctypes.byref(ptr), ctypes.byref(nb))
+            x = torch.empty(nb.value // torch.tensor([], dtype=dt).element_size(), dtype=dt, device="cuda")
+            eng.rollout_copy(name, x)
+            out.append(x.view(E, 2, rc)[:, :, :N].contiguous() if name in ("actions", "rewards") else x)
+        for g in range(2):
+            for name, w in (("view", 13 * 13 * 7), ("feature", 34)):
+                x = torch.empty(E * rc * w, dtype=torch.float32, device="cuda")
+                eng.rollout_copy(name, x, group=g)
+                out.append(x.view(E, rc, w)[:, :N].contiguous())
+        return out
+
+    for n in (13, 30):
+        for eng in engs:
+            eng.rollout_step(n)
+        for eng in engs:
+            eng.rollout_check()
+        ref = dump(engs[0])
+        for j, other in enumerate(engs[1:]):
+            got = dump(other)
+            torch.cuda.synchronize()
+            for k, (x, y) in enumerate(zip(ref, got)):
+                if not torch.equal(x.view(torch.uint8), y.view(torch.uint8)):
+                    bad = (x.view(torch.uint8) != y.view(torch.uint8)).view(x.shape[0], x.shape[1], -1).any(-1)
+                    idx = bad.nonzero()[:12].tolist()
+                    gn = ref[5].view(E, 2).tolist()
+                    raise AssertionError((n, k, j, idx, [gn[i[0]] for i in idx], int(bad.sum())))
+            del got
+        del ref
 
 
 @pytest.mark.parametrize("sub", [2, 7])
