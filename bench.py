@@ -53,8 +53,10 @@ def parse(argv=None):
     # launch ramp-up / tail and the env install / write-back are paid once per 4 steps, +9-11 % over one
     # step per launch; 8 and 16 gain nothing more (profiles/r02_substeps_sweep.txt).  The results are
     # bit-identical for any value (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps).
-    ap.add_argument("--substeps", type=int, default=4,
-                    help="consecutive steps of every env per k_rollout launch (env image kept in LDS)")
+    # Large envs (256x256, k_rollout_bigq): 8 steps per launch, 1.06-1.10e9 against 1.0-1.07e9 at 4 (the
+    # launch's tail is the last envs' steps; profiles/r02_bigq_sweeps.txt).
+    ap.add_argument("--substeps", type=int, default=None,
+                    help="consecutive steps of every env per launch (default 4 at 64x64, 8 for large maps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -69,6 +71,8 @@ def parse(argv=None):
         # and the tail of the persistent grid), amortised over more envs: at 4 steps per launch 24576 ->
         # 32768 -> 49152 envs = 1.09 -> 1.137 -> 1.146e9 agent-steps/s (profiles/r02_env_sub_sweep.txt)
         a.envs = 49152 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
+    if a.substeps is None:
+        a.substeps = 4 if a.map * a.map <= 64 * 64 else 8
     return a
 
 
@@ -257,8 +261,8 @@ def main():
     S = max(1, args.substeps)
     if S != 1:
         eng.rollout_substeps(S)
-    grid, _ = eng.rollout_info()
-    big = grid == E and args.map * args.map > 64 * 64     # k_observe_items + k_rollout_big (state in HBM)
+    grid, lds = eng.rollout_info()
+    big = args.map * args.map > 64 * 64 and lds > 64 * 1024   # large envs, state in HBM (k_rollout_bigq)
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")
 
@@ -321,7 +325,7 @@ def main():
             if pm.get("envs") == E and pm.get("map", MAP) == args.map and pm.get("substeps", 1) == S:
                 traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_step"))
         strong = args.total_envs is not None
-        kern = "k_observe_items+k_rollout_big" if big else "k_rollout"
+        kern = "k_rollout_bigq" if big else "k_rollout"
         line = {
             "metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents" % (args.map, args.map, args.agents),
             "value": total_units / elapsed,
@@ -337,7 +341,7 @@ def main():
                        % (args.map, args.map, args.agents // 2, args.agents // 2,
                           ("%d envs over %d GPUs" % (args.total_envs, world)) if strong else "%d envs per GPU" % E,
                           args.max_steps,
-                          "k_observe_items + k_rollout_big on 2 streams" if big else
+                          ("queue-driven k_rollout_bigq, %d steps per launch" % S) if big else
                           ("fused step" if S == 1 else "fused step, %d consecutive steps per launch" % S)),
                        "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S,
                        "parallelism": "envs sharded one process per GPU (dp%d)" % world},
@@ -345,7 +349,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kernel_ms,
                          "kernel_ms_is": "mean launch duration (HIP events on the launch stream), %d step(s) per launch"
-                                         % S if not big else "mean span of one step over its streams (HIP events)",
+                                         % S,
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch},
             "cpu_baseline": None,
             "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],

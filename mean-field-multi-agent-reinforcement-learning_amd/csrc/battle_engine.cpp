@@ -242,7 +242,7 @@ public:
     // k_observe_items slots, leaving room for the other stream's step.  Measured at 256x256 / 4096
     // agents, 1024 envs (profiles/r01_big_sweeps.txt): 2 streams / 1/3 grid / 64-agent items best.
     static constexpr int kBigSplit = 2, kItemGridDiv = 3, kItemRows = 64;
-    static constexpr int kBigqRows = 64;          // agents per k_rollout_bigq observation item
+    static constexpr int kBigqRows = 512;         // agents per k_rollout_bigq observation item (64: 9.6e8, 256: 1.06e9, 384-512: 1.08e9, 1024: 1.04e9; profiles/r02_bigq_sweeps.txt)
     static constexpr bool kPipeDefault = false;   // measured slower than the fused step
     static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
@@ -1182,9 +1182,9 @@ public:
                     ro_bigq = ro_bigq && ro_q_grid > 0;          // (0: not one SPX device of 8 XCDs)
                     if (ro_bigq) {
                         // per list and parity: one filing per env and step of a launch (<= 64 steps)
-                        // (+ the tickets idle workgroups hold past the last filing: one per workgroup)
+                        // (+ the tickets workgroups hold past the last filing: two per workgroup)
                         const size_t lcap = (size_t)((E + kXcds - 1) / kXcds) * 64 * (size_t)(n_groups() * chunks) +
-                                            (size_t)ro_q_grid;
+                                            2 * (size_t)ro_q_grid;
                         ro_q_items.ensure(2 * kXcds * lcap);
                         ro_q_cnt.ensure(2 * kXcds * kObsCntPad);
                         ro_q_left.ensure(E); ro_q_si.ensure(E); ro_q_done.ensure(kObsCntPad);
