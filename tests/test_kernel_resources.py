@@ -50,3 +50,17 @@ def test_hot_kernels_do_not_spill():
             u = usage[k]
             assert u.get("VGPRs Spill", 0) == 0, (name, u)
             assert u.get("ScratchSize", 0) == 0, (name, u)
+
+
+def test_queue_kernel_register_budget():
+    """k_rollout_bigq (the large-env bench kernel) inlines the step into the item loop: two 512-lane
+    workgroups per CU (4 waves per SIMD, <= 128 VGPRs) with a few spills inside the step (72 B of
+    scratch per lane).  The step as a real call needed 436 B of stack per lane and ran 11 % slower
+    (profiles/r02_bigq_sweeps.txt); this bounds both."""
+    usage = _usage()
+    hits = [k for k in usage if k.startswith("_ZN3mfx14k_rollout_bigq")]
+    assert hits
+    for k in hits:
+        u = usage[k]
+        assert u.get("VGPRs", 999) <= 128, u
+        assert u.get("ScratchSize", 0) <= 96, u
