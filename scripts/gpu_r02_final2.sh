@@ -3,7 +3,7 @@
 # and FETCH_SIZE / WRITE_SIZE passes, the 2-rank launcher rehearsal and configs[3].
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r02h
+O=${OUT:-gpurun_out/r02h}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
