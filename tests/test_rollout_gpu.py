@@ -484,6 +484,53 @@ def test_rollout_large_env_queue_matches_pipeline(monkeypatch):
         del ref
 
 
+def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
+    """The 256x256 bench's own shape (configs[4]: 1024 staggered envs of 2048 + 2048 agents, episode cap
+    400, 8 steps per k_rollout_bigq launch) against the two-stream pipeline at one step per launch,
+    after 408 steps (every env restarts at least once, inside a launch for most): every output
+    buffer bit for bit (all rows the first step wrote), the episode statistics, the agent-step
+    counters, and no stalled queue."""
+    import ctypes
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, M, N, T = 1024, 256, 2048, 408
+    left, right = bd.block_positions(M, N)
+    engs = []
+    for fused, sub in (("0", 1), ("1", 8)):
+        monkeypatch.setenv("MFX_BIG_FUSED", fused)
+        eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1234, stagger=True)
+        eng.rollout_substeps(sub)
+        eng.rollout_step(T)
+        engs.append(eng)
+    engs[1].rollout_check()
+    rc = engs[0].rowcap
+    for name, dt in (("actions", torch.int32), ("rewards", torch.float32), ("mean_action", torch.float64),
+                     ("stats", torch.float64), ("agent_steps", torch.int64), ("group_num", torch.int32),
+                     ("episode_return", torch.float32)):
+        xs = []
+        for eng in engs:
+            ptr, nb = ctypes.c_void_p(), ctypes.c_size_t()
+            eng._dll.mfx_battle_rollout_buffer(eng.game, name.encode(), 0, ctypes.byref(ptr), ctypes.byref(nb))
+            x = torch.empty(nb.value // torch.tensor([], dtype=dt).element_size(), dtype=dt, device="cuda")
+            eng.rollout_copy(name, x)
+            xs.append(x.view(E, 2, rc)[:, :, :N] if name in ("actions", "rewards") else x)
+        torch.cuda.synchronize()
+        assert torch.equal(xs[0].view(torch.uint8) if xs[0].is_contiguous() else xs[0].contiguous().view(torch.uint8),
+                           xs[1].view(torch.uint8) if xs[1].is_contiguous() else xs[1].contiguous().view(torch.uint8)), name
+    for g in range(2):
+        for name, w in (("feature", 34), ("view", 13 * 13 * 7)):
+            xs = []
+            for eng in engs:
+                x = torch.empty(E * rc * w, dtype=torch.float32, device="cuda")
+                eng.rollout_copy(name, x, group=g)
+                xs.append(x.view(E, rc, w)[:, :N])
+            torch.cuda.synchronize()
+            same = torch.equal(xs[0].view(torch.int32), xs[1].view(torch.int32))
+            assert same, (name, g, int((xs[0].view(torch.int32) != xs[1].view(torch.int32)).any(-1).sum()))
+            del xs
+
+
 @pytest.mark.parametrize("sub", [2, 7])
 def test_rollout_substeps_match_single_steps(sub):
     """k_rollout running `sub` consecutive steps of each env per launch (image kept in LDS) leaves
