@@ -299,8 +299,9 @@ hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, int* gri
     if (err == hipSuccess)
         err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rollout_bigq, kBigRolloutThreads, smem);
     if (err != hipSuccess) return err;
-    // one device of 8 XCDs (SPX): every XCD gets workgroups of the full-occupancy grid (k_rollout_bigq)
-    *grid = (cus % kXcds == 0 && cus >= 8 * kXcds) ? cus * (per_cu > 0 ? per_cu : 1) : 0;
+    // one device of all 8 XCDs (SPX, 32 CUs each): every XCD gets workgroups of the full-occupancy grid,
+    // and the XCC ids are 0-7 (k_rollout_bigq keeps each env on XCD e % 8)
+    *grid = (cus % kXcds == 0 && cus >= 32 * kXcds) ? cus * (per_cu > 0 ? per_cu : 1) : 0;
     return hipSuccess;
 }
 
