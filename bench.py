@@ -53,10 +53,10 @@ def parse(argv=None):
     # launch ramp-up / tail and the env install / write-back are paid once per 4 steps, +9-11 % over one
     # step per launch; 8 and 16 gain nothing more (profiles/r02_substeps_sweep.txt).  The results are
     # bit-identical for any value (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps).
-    # Large envs (256x256, k_rollout_bigq): 8 steps per launch, 1.06-1.10e9 against 1.0-1.07e9 at 4 (the
-    # launch's tail is the last envs' steps; profiles/r02_bigq_sweeps.txt).
+    # Large envs (256x256, k_rollout_bigq): 16 steps per launch (the launch's tail is the last envs'
+    # steps): 1.19-1.20e9 against 1.15-1.18e9 at 8 and 1.0-1.07e9 at 4 (profiles/r02_bigq_sweeps.txt).
     ap.add_argument("--substeps", type=int, default=None,
-                    help="consecutive steps of every env per launch (default 4 at 64x64, 8 for large maps)")
+                    help="consecutive steps of every env per launch (default 4 at 64x64, 16 for large maps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -72,7 +72,7 @@ def parse(argv=None):
         # 32768 -> 49152 envs = 1.09 -> 1.137 -> 1.146e9 agent-steps/s (profiles/r02_env_sub_sweep.txt)
         a.envs = 49152 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
     if a.substeps is None:
-        a.substeps = 4 if a.map * a.map <= 64 * 64 else 8
+        a.substeps = 4 if a.map * a.map <= 64 * 64 else 16
     return a
 
 
