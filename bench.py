@@ -19,6 +19,13 @@ rank; run directly with --gpus N > 1 it starts N fresh rank processes itself (be
 touches the GPU) and exits with their status.  --envs E: E envs per rank (weak scaling);
 --total-envs T: T envs split over the ranks (strong scaling, configs[3]: 64 envs over 8 GPUs).
 The only collective is the RCCL all-reduce of the episode statistics.
+
+Self-check (after the clock, outside the timed region): every rank replays --check-envs sampled envs of
+its own batch on the C oracle from rollout_init on (tests/rollout_check.py: the oracle steps with a host
+restatement of the device's counter-hash rush policy) and compares the last step's observation, actions,
+rewards and mean action, the state after it (ids, positions, hp), and the env's counters (agent-steps,
+episode statistics, running return) bit for bit; it also reads the device and queue error words
+(rollout_check).  The line's "check" records it; a mismatch exits non-zero.
 """
 import argparse
 import json
@@ -65,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--backend", default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher self-test only
+    ap.add_argument("--check-envs", type=int, default=8,
+                    help="envs per rank replayed on the C oracle after the timed region (0: no check)")
     a = ap.parse_args(argv)
     if a.envs is None and a.total_envs is None:
         # 64x64: 49152 envs per GPU (~60 GB of observation buffers) -- a launch has a fixed cost (ramp-up
@@ -116,6 +126,9 @@ def launch_ranks(n, argv):
                 for q in live:
                     q.terminate()
         time.sleep(0.05)
+    if status:
+        for r, p in enumerate(procs):
+            sys.stderr.write("bench launcher: rank %d exited %d\n" % (r, p.returncode))
     return status
 
 
@@ -129,6 +142,17 @@ def launcher_selftest(args):
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
+    if world > 1 and args.fail_rank >= 0:
+        # a rank that dies while the others wait in a collective: rank fail_rank exits 3 once every other
+        # rank has announced (through the rendezvous store) that it is entering the barrier
+        store = dist.distributed_c10d._get_default_store()
+        if rank == args.fail_rank:
+            store.wait(["entering%d" % r for r in range(world) if r != rank])
+            time.sleep(0.3)
+            os._exit(3)
+        store.set("entering%d" % rank, "1")
+        dist.barrier()                       # never completes: the launcher must stop this rank
+        return
     E = rank_envs(args, world, rank)
     red = reduce_stats(torch.ones(E, 4, dtype=torch.float64)).tolist()
     elapsed, units = reduce_timing(0.01 * (rank + 1), 100 * (rank + 1), "cpu")
@@ -226,6 +250,38 @@ def run_cpu_baseline(seconds, map_size, agents, procs=None):
                                      res[0]["lib"])}
 
 
+# ----------------------------------------------------------------------------- self-check
+def run_check(eng, args, E, placement, seed, world):
+    """Replay args.check_envs sampled envs of this rank's batch on the C oracle from rollout_init through
+    the preparation, warmup and timed steps (tests/rollout_check.py); all ranks' verdicts reduced."""
+    if args.check_envs <= 0:
+        return None
+    import torch
+    import torch.distributed as dist
+    import rollout_check as rc
+    steps = args.max_steps + args.warmup + args.steps            # every step since rollout_init
+    envs = rc.sample_envs(E, args.check_envs)
+    t = time.perf_counter()
+    err = None
+    try:
+        chk = rc.RolloutChecker(eng, args.map, placement, envs, args.max_steps, True, seed, 0.2)
+        bad = chk.check(steps)
+    except Exception as x:                  # a device / queue error word (rollout_check) or a failed read
+        bad, err = ["%s: %s" % (type(x).__name__, x)], True
+    ok = torch.tensor([0.0 if bad else 1.0], dtype=torch.float64, device="cuda")
+    n = torch.tensor([float(len(envs))], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        dist.all_reduce(n)
+    return {"ok": bool(ok.item() == 1.0), "envs": int(n.item()), "envs_per_rank": len(envs), "steps": steps,
+            "sample_rank0": envs, "path": eng.rollout_path() if err is None else None,
+            "what": "each sampled env replayed from rollout_init on the C oracle (oracle/battle_oracle.c) with a "
+                    "host restatement of the device rush policy; last step's views, features, actions, rewards, "
+                    "mean action, post-step ids / positions / hp, agent-steps, episode statistics and return "
+                    "compared bit for bit; device and queue error words read (rollout_check); after the clock",
+            "seconds": time.perf_counter() - t, "mismatches": bad[:16]}
+
+
 # ----------------------------------------------------------------------------- GPU bench
 def main():
     args = parse()
@@ -261,8 +317,8 @@ def main():
     S = max(1, args.substeps)
     if S != 1:
         eng.rollout_substeps(S)
-    grid, lds = eng.rollout_info()
-    big = args.map * args.map > 64 * 64 and lds > 64 * 1024   # large envs, state in HBM (k_rollout_bigq)
+    path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
+    big = path in ("k_rollout_bigq", "k_observe_items+k_rollout_big")   # large envs, state in HBM
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")
 
@@ -313,6 +369,7 @@ def main():
     kernel_ms = sum(full) / len(full)
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
+    check = run_check(eng, args, E, [left, right], env_seed(1234, rank), world)
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         units_per_launch = local_units / args.steps * S
@@ -325,7 +382,7 @@ def main():
             if pm.get("envs") == E and pm.get("map", MAP) == args.map and pm.get("substeps", 1) == S:
                 traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_step"))
         strong = args.total_envs is not None
-        kern = "k_rollout_bigq" if big else "k_rollout"
+        kern = {"k_rollout_obs+k_rollout": "k_rollout"}.get(path, path)
         line = {
             "metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents" % (args.map, args.map, args.agents),
             "value": total_units / elapsed,
@@ -341,7 +398,7 @@ def main():
                        % (args.map, args.map, args.agents // 2, args.agents // 2,
                           ("%d envs over %d GPUs" % (args.total_envs, world)) if strong else "%d envs per GPU" % E,
                           args.max_steps,
-                          ("queue-driven k_rollout_bigq, %d steps per launch" % S) if big else
+                          ("%s, %d steps per launch" % (path, S)) if big else
                           ("fused step" if S == 1 else "fused step, %d consecutive steps per launch" % S)),
                        "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S,
                        "parallelism": "envs sharded one process per GPU (dp%d)" % world},
@@ -355,11 +412,16 @@ def main():
             "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],
                          "kills": red[3], "note": "all ranks, since rollout_init (RCCL all-reduce per episode batch)"},
         }
+        if check is not None:
+            line["check"] = check
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = run_cpu_baseline(args.cpu_seconds, args.map, args.agents, args.cpu_procs)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if check is not None and not check["ok"]:
+        sys.stderr.write("bench self-check FAILED: %s\n" % check["mismatches"][:8])
+        return 1
     return 0
 
 

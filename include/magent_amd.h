@@ -123,9 +123,13 @@ int mfx_battle_rollout_copy_at(void *game, const char *name, int group, size_t o
 int mfx_battle_rollout_rowcap(void *game, int *rowcap);
 /* Persistent grid (workgroups per launch) and dynamic LDS bytes per workgroup of the fused rollout. */
 int mfx_battle_rollout_info(void *game, int *grid, int *lds_bytes);
-/* Large envs: -1 (message in mfx_last_error) if the in-launch work queue of k_rollout_bigq ever
- * stalled; synchronises the engine stream. */
+/* Synchronises the engine stream; -1 (message in mfx_last_error) if a device error was raised or, on the
+ * large-env queue kernel k_rollout_bigq, its work queue reported an error (a stall, a workgroup outside
+ * XCDs 0-7, or the hand-off guard: an item that saw a step counter other than its own). */
 int mfx_battle_rollout_check(void *game);
+/* The kernels rollout_step runs: 0 k_rollout, 1 k_rollout_obs + k_rollout (pipeline), 2 k_observe_items +
+ * k_rollout_big (large-env pipeline), 3 k_rollout_bigq. */
+int mfx_battle_rollout_path(void *game, int *path);
 /* Diagnostic build only (libmagent_stamps.so): per-phase s_memtime stamps [E][16]. */
 int mfx_battle_set_stamp_buffer(void *d_buf);
 

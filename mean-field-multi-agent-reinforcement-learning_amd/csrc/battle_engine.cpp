@@ -218,7 +218,7 @@ public:
     DevBuf<int32_t> ro_q_cnt, ro_q_left, ro_q_done;
     int ro_q_grid = 0, ro_qpar = 0;
     uint32_t ro_qlaunch = 0, ro_qdone = 0;   // launches so far (item tags); env-steps the queue has done
-    static uint32_t qtag(uint32_t launch) { return launch % 4095u + 1u; }
+    static uint32_t qtag(uint32_t launch) { return launch % 63u + 1u; }   // 6 tag bits (rollout_big.inc), never 0
     bool ro_prep_stale = true;               // ro_mm / ro_info / items lag the state (per-call calls since)
     DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
     DevBuf<double> ro_mean, ro_stats;
@@ -1194,7 +1194,9 @@ public:
                         ra.q_si = ro_q_si.p; ra.q_done = ro_q_done.p; ra.q_list_cap = lcap;
                         ra.obs_item_rows = Rq;
                         const char* qg = getenv("MFX_BIGQ_GRID");               // sweeps only
-                        if (qg && atoi(qg) > 0) ro_q_grid = std::min(ro_q_grid, atoi(qg));
+                        // (a multiple of kXcds: every XCD's list needs workgroups of its own)
+                        if (qg && atoi(qg) > 0)
+                            ro_q_grid = std::min(ro_q_grid, std::max(kXcds, atoi(qg) - atoi(qg) % kXcds));
                     }
                 } else {
                     ro_bigq = false;
@@ -1258,8 +1260,13 @@ public:
             MFX_CHECK(sync_cells());
             const size_t lst = (size_t)kXcds * kObsCntPad;           // counters of one parity
             if (ro_prep_stale) {
+                // Re-seed after per-call calls: the last launch's filings for the next launch (never
+                // consumed) still hold the live tag in the slots past the new, smaller filing count --
+                // clear every slot and move to a fresh tag, so no stale word can pass for an item.
                 ro_qpar = 0;
                 ro_qdone = 0;
+                ro_qlaunch++;
+                MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, 2 * lst * sizeof(int32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
                 MFX_HIP(launch_bigq_seed(d_gp, s, ra, ro_qpar, qtag(ro_qlaunch), ra.step_index, stream));
@@ -1348,15 +1355,27 @@ public:
         return 0;
     }
 
-    // The queue-driven large-env kernel's error word (a queue that stopped making progress): 0 if none.
+    // Synchronise and report the device error word and, on the queue-driven large-env kernel, its queue
+    // error word: 0 if neither is set.
     int rollout_check() {
         if (!rollout_ready) return fail("rollout_check before rollout_init");
-        if (!(ro_big && ro_bigq)) return 0;
-        int32_t w[kObsCntPad] = {};
-        MFX_HIP(hipMemcpyAsync(w, ro_q_done.p, sizeof(w), hipMemcpyDeviceToHost, stream));
-        MFX_HIP(hipStreamSynchronize(stream));
-        if (w[2]) return fail("rollout: the large-env work queue stalled (code %d)", w[2]);
-        return 0;
+        if (ro_big && ro_bigq) {
+            int32_t w[kObsCntPad] = {};
+            MFX_HIP(hipMemcpyAsync(w, ro_q_done.p, sizeof(w), hipMemcpyDeviceToHost, stream));
+            MFX_HIP(hipStreamSynchronize(stream));
+            static const char* msg[] = {"", "", "a wait without progress (stalled queue)", "a ticket past the list",
+                                        "a workgroup outside XCDs 0-7 (not one SPX device)",
+                                        "hand-off guard: an item saw a step counter other than its own"};
+            if (w[2]) return fail("rollout: k_rollout_bigq error %d: %s", w[2], w[2] > 0 && w[2] < 6 ? msg[w[2]] : "?");
+        }
+        return check_err();
+    }
+
+    // Which kernels rollout_step runs (include/magent_amd.h mfx_battle_rollout_path).
+    int rollout_path() const {
+        if (!rollout_ready) return -1;
+        if (ro_big) return ro_bigq ? 3 : 2;
+        return ro_pipe ? 1 : 0;
     }
 
     int rollout_info(int* grid, int* lds_bytes) {
@@ -2211,14 +2230,25 @@ MFX_API int mfx_battle_rollout_info(void* game, int* grid, int* lds_bytes) {
     MFX_GUARD(MFX_ENV(game)->rollout_info(grid, lds_bytes));
 }
 
-// Large envs (k_rollout_bigq): -1 and the message if the in-launch work queue ever stalled (syncs).
+// Synchronise; -1 and the message if a device error was raised or (k_rollout_bigq) the in-launch work
+// queue reported an error.
 MFX_API int mfx_battle_rollout_check(void* game) {
     MFX_GUARD(MFX_ENV(game)->rollout_check());
 }
+// The kernels rollout_step runs: 0 k_rollout, 1 k_rollout_obs + k_rollout (pipeline), 2 k_observe_items +
+// k_rollout_big (large-env pipeline), 3 k_rollout_bigq.
+MFX_API int mfx_battle_rollout_path(void* game, int* path) {
+    const int p = MFX_ENV(game)->rollout_path();
+    if (p < 0) return mfx::fail("rollout_path before rollout_init");
+    *path = p;
+    return 0;
+}
 
 // Steps per k_rollout launch (1..64): every env runs that many consecutive steps while its image stays
-// in LDS.  rollout_step(n) results are identical for any value (the last step's buffers, the same
-// state); only the launch count changes.  Ignored by the pipeline and the large-env path.
+// in LDS; the large-env queue kernel k_rollout_bigq runs that many steps of every env per launch (its
+// item lists hold one filing per env and step of a launch: lcap in rollout_plan, hence <= 64).
+// rollout_step(n) results are identical for any value (the last step's buffers, the same state); only
+// the launch count changes.  Ignored by the two pipelines (one step per launch).
 MFX_API int mfx_battle_rollout_set_substeps(void* game, int n_sub) {
     if (n_sub < 1 || n_sub > 64) return mfx::fail("rollout_set_substeps: %d not in 1..64", n_sub);
     MFX_ENV(game)->ro_sub = n_sub;

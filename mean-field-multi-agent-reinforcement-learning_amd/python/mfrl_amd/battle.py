@@ -32,7 +32,7 @@ class BattleBatch:
                    "mfx_battle_sync", "mfx_battle_rollout_init", "mfx_battle_rollout_step",
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
-                   "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check"):
+                   "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check", "mfx_battle_rollout_path"):
             try:
                 getattr(self._dll, fn).restype = ctypes.c_int
             except AttributeError:          # an older build of the library (A/B runs)
@@ -116,8 +116,17 @@ class BattleBatch:
         return g.value, b.value
 
     def rollout_check(self):
-        """Raise if the large-env queue kernel (k_rollout_bigq) ever stalled (synchronises)."""
+        """Synchronise; raise on a device error word or an error of the large-env queue kernel
+        (k_rollout_bigq: a stall, a workgroup outside XCDs 0-7, the hand-off guard)."""
         self._check(self._dll.mfx_battle_rollout_check(self.game), "rollout_check")
+
+    PATHS = ("k_rollout", "k_rollout_obs+k_rollout", "k_observe_items+k_rollout_big", "k_rollout_bigq")
+
+    def rollout_path(self):
+        """Name of the kernels rollout_step runs (the path rollout_init / the last re-plan chose)."""
+        p = ctypes.c_int()
+        self._check(self._dll.mfx_battle_rollout_path(self.game, ctypes.byref(p)), "rollout_path")
+        return self.PATHS[p.value]
 
     def rollout_substeps(self, n_sub):
         """Consecutive steps of every env per k_rollout launch (results do not depend on it)."""

@@ -650,6 +650,12 @@ int env_get_info(void *game, int group, const char *name, void *buffer) {   /* G
         for (int i = 0; i < e->groups[group].n; i++) bb[i] = !e->pool[e->groups[group].ids[i]].dead;
         return 0;
     }
+    /* not a reference key: the hp of every group member (the rollout replays compare the state with it) */
+    if (!strcmp(name, "hp")) {
+        float *fb = buffer;
+        for (int i = 0; i < e->groups[group].n; i++) fb[i] = e->pool[e->groups[group].ids[i]].hp;
+        return 0;
+    }
     if (!strcmp(name, "action_space")) { ib[0] = gtype(e, group)->n_action; return 0; }
     if (!strcmp(name, "view_space")) {
         ib[0] = gtype(e, group)->view.h; ib[1] = gtype(e, group)->view.w; ib[2] = group2channel(e, e->n_groups);

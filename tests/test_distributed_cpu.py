@@ -67,14 +67,22 @@ def test_bench_launcher_spawns_ranks(world, total):
 
 
 def test_bench_launcher_propagates_failure():
-    """A rank that fails makes the launcher fail (and stops the other ranks)."""
+    """A rank that dies while the other waits in a collective: rank 1 exits 3 only after rank 0 has
+    announced (rendezvous store) that it is entering a gloo barrier it can never leave.  The launcher
+    must return non-zero well within the timeout and have terminated rank 0 (SIGTERM)."""
     import subprocess
     import sys
+    import time
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t = time.time()
     out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launcher-selftest",
-                          "--no-such-flag"], env=env, capture_output=True, text=True, timeout=120)
-    assert out.returncode != 0
+                          "--backend", "gloo", "--fail-rank", "1"], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 3, (out.returncode, out.stderr[-2000:])
+    assert time.time() - t < 90
+    assert "rank 1 exited 3" in out.stderr, out.stderr[-2000:]
+    assert "rank 0 exited -15" in out.stderr, out.stderr[-2000:]     # stopped by the launcher, not finished
 
 
 def test_cpu_baseline_uses_several_cores():

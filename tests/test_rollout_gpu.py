@@ -8,6 +8,7 @@ import pytest
 
 import battle_driver as bd
 import common
+import rollout_check as rck
 
 pytestmark = pytest.mark.gpu
 
@@ -118,6 +119,7 @@ def test_rollout_large_env_matches_oracle(map_size, n_side, E, T, max_steps):
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=5, stagger=False)
     grid, lds = eng.rollout_info()
     assert grid == E and lds > 64 * 1024          # the large-env path was chosen
+    assert eng.rollout_path() == "k_rollout_bigq"
     rc = eng.rowcap
     VF, F = 13 * 13 * 7, 34
     envs = []
@@ -291,73 +293,54 @@ def _sample_envs(E, k=16):
     return sorted(set([0, 1, E // 2, E - 2, E - 1] + [int(x) for x in np.linspace(0, E - 1, k - 5)]))[:k]
 
 
+def _check_launches(eng, map_size, n_side, envs, T, S, max_steps, seed, eps, path):
+    """Run T steps as launches of S steps; after EVERY launch compare the sampled envs with their oracle
+    replays (tests/rollout_check.py: last step's observation / actions / rewards / mean action, the state
+    after it, agent-steps, episode statistics, running return; device and queue error words)."""
+    assert eng.rollout_path() == path, eng.rollout_path()
+    chk = rck.RolloutChecker(eng, map_size, bd.block_positions(map_size, n_side), envs, max_steps, True, seed, eps)
+    restarts_before = [r.stats[0] for r in chk.replays]
+    t = 0
+    while t < T:
+        k = min(S, T - t)
+        eng.rollout_step(k)
+        t += k
+        bad = chk.check(t)
+        assert not bad, bad[:8]
+    assert all(r.stats[0] > b for r, b in zip(chk.replays, restarts_before))     # every sampled env restarted
+
+
 def test_rollout_bench_shape_matches_oracle():
-    """The bench's own batch shape: 4096 staggered envs (the persistent grid is smaller than E, so the
-    heaviest-first class queue, the register prefetch of the next env and the queue hand-off are all
-    live), 450 steps (every env restarts at least once).  16 sampled envs are replayed on the C oracle
-    step by step with the actions the device policy chose: views, features, rewards and the mean action
-    bit for bit.  Stagger: env e's first episode starts at length e * max_steps // E
-    (BattleEngine::rollout_init)."""
+    """The 64x64 bench exactly as bench.py runs it: 49152 staggered envs (the persistent grid is far
+    smaller than E, so the heaviest-first class queue, the register prefetch and the queue hand-off are
+    live), 4 steps per k_rollout launch, 452 steps (every env restarts at least once; the bench's
+    preparation + warmup + timed window is 425).  16 sampled envs are replayed on the C oracle from
+    rollout_init on with the host restatement of the device rush policy, and compared after every launch.
+    Stagger: env e's first episode starts at length e * max_steps // E (BattleEngine::rollout_init)."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, T, max_steps, VF, F = 4096, 450, 400, 13 * 13 * 7, 34
+    E, T, S, max_steps, seed = 49152, 452, 4, 400, 1234
     left, right = bd.block_positions(64, 128)
     eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
-    eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=1234, stagger=True)
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
+    eng.rollout_substeps(S)
     grid, _ = eng.rollout_info()
     assert grid < E                                  # the work queue hands out envs
-    rc = eng.rowcap
-    sample = _sample_envs(E)
-    envs = []
-    for e in sample:
-        env, h = common.battle_env(common.ORACLE_LIB, 64)
-        env.reset()
-        env.add_agents(h[0], method="custom", pos=left)
-        env.add_agents(h[1], method="custom", pos=right)
-        envs.append([env, h, e * max_steps // E])
-    view = torch.empty((len(sample), 2, rc, VF), dtype=torch.float32).pin_memory()
-    feat = torch.empty((len(sample), 2, rc, F), dtype=torch.float32).pin_memory()
-    act = torch.empty((len(sample), 2, rc), dtype=torch.int32).pin_memory()
-    rew = torch.empty((len(sample), 2, rc), dtype=torch.float32).pin_memory()
-    mean = torch.empty((len(sample), 2, 21), dtype=torch.float64).pin_memory()
-    restarts = 0
-    for t in range(T):
-        eng.rollout_step(1)
-        for j, e in enumerate(sample):
-            for g in range(2):
-                eng.rollout_copy_at("view", view[j, g], e * rc * VF * 4, group=g)
-                eng.rollout_copy_at("feature", feat[j, g], e * rc * F * 4, group=g)
-            eng.rollout_copy_at("actions", act[j], e * 2 * rc * 4)
-            eng.rollout_copy_at("rewards", rew[j], e * 2 * rc * 4)
-            eng.rollout_copy_at("mean_action", mean[j], e * 2 * 21 * 8)
-        eng.sync()
-        for j, st in enumerate(envs):
-            env, h, _ = st
-            acts = []
-            for g in range(2):
-                v, f = env.get_observation(h[g])
-                n = len(v)
-                assert view[j, g, :n].numpy().tobytes() == v.reshape(n, VF).tobytes(), (sample[j], t, g, "view")
-                assert feat[j, g, :n].numpy().tobytes() == f.tobytes(), (sample[j], t, g, "feature")
-                a = act[j, g, :n].numpy().astype(np.int32)
-                acts.append(a)
-                m = np.mean(list(map(lambda x: np.eye(21)[x], a)), axis=0) if n else np.full(21, np.nan)
-                assert np.array_equal(mean[j, g].numpy(), m, equal_nan=True), (sample[j], t, g, "mean")
-            for g in range(2):
-                env.set_action(h[g], acts[g])
-            done = env.step()
-            for g in range(2):
-                rw = env.get_reward(h[g])
-                assert rew[j, g, :len(rw)].numpy().tobytes() == rw.tobytes(), (sample[j], t, g, "reward")
-            env.clear_dead()
-            st[2] += 1
-            if done or st[2] >= max_steps:
-                st[2] = 0
-                restarts += 1
-                env.reset()
-                env.add_agents(h[0], method="custom", pos=left)
-                env.add_agents(h[1], method="custom", pos=right)
-    assert restarts >= len(sample)
+    _check_launches(eng, 64, 128, _sample_envs(E), T, S, max_steps, seed, 0.2, "k_rollout")
+
+
+def test_rollout_bigq_bench_shape_matches_oracle():
+    """The 256x256 bench (configs[4]) exactly as bench.py runs it: 1024 staggered envs of 2048 + 2048
+    agents, 16 steps per k_rollout_bigq launch, 416 steps (every env restarts, most inside a launch).
+    8 sampled envs replayed on the C oracle from rollout_init on, compared after every launch."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, T, S, max_steps, seed = 1024, 416, 16, 400, 1234
+    left, right = bd.block_positions(256, 2048)
+    eng = BattleBatch(256, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
+    eng.rollout_substeps(S)
+    _check_launches(eng, 256, 2048, _sample_envs(E, 8), T, S, max_steps, seed, 0.2, "k_rollout_bigq")
 
 
 def test_rollout_large_env_staggered_many_envs_matches_oracle():
@@ -374,6 +357,7 @@ def test_rollout_large_env_staggered_many_envs_matches_oracle():
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=99, stagger=True)
     grid, lds = eng.rollout_info()
     assert lds > 64 * 1024                           # the large-env path
+    assert eng.rollout_path() == "k_rollout_bigq"
     rc = eng.rowcap
     envs = []
     for e in range(E):
@@ -444,6 +428,7 @@ def test_rollout_large_env_queue_matches_pipeline(monkeypatch):
         eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
         eng.rollout_init([left, right], max_steps=24, eps=0.3, seed=41, stagger=True)
         eng.rollout_substeps(sub)
+        assert eng.rollout_path() == ("k_rollout_bigq" if fused == "1" else "k_observe_items+k_rollout_big")
         engs.append(eng)
 
     N = 1250                 # rows every env wrote at its first step (the rows past them were never written)
@@ -484,9 +469,77 @@ def test_rollout_large_env_queue_matches_pipeline(monkeypatch):
         del ref
 
 
+def test_rollout_bigq_reseed_after_per_call_ops(monkeypatch):
+    """Per-call calls between queue-kernel launches: after an even number of launches the
+    last launch's filings for the next launch sit unconsumed in parity 0 under the live tag; per-call
+    steps with attacks and clear_dead shrink the groups, so the re-seed files fewer items than those
+    slots hold.  The re-seed must clear them (or k_rollout_bigq would take stale words for items).
+    32-agent items (MFX_BIGQ_ROWS), so a few deaths change the filing counts.  Checked against the
+    two-stream pipeline given the same per-call calls: every output buffer, the statistics and counters
+    bit for bit, and no queue error."""
+    import ctypes
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, M, S, R = 24, 200, 5, 32
+    left, right = bd.block_positions(M, 1250)
+    monkeypatch.setenv("MFX_BIGQ_ROWS", str(R))
+    engs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("MFX_BIG_FUSED", fused)
+        eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=60, eps=0.3, seed=17, stagger=True)
+        eng.rollout_substeps(S)
+        engs.append(eng)
+    assert engs[1].rollout_path() == "k_rollout_bigq"
+    rc = engs[0].rowcap
+
+    def dump(eng):
+        out = []
+        for name, dt in (("actions", torch.int32), ("rewards", torch.float32), ("mean_action", torch.float64),
+                         ("stats", torch.float64), ("agent_steps", torch.int64), ("group_num", torch.int32),
+                         ("episode_return", torch.float32)):
+            ptr, nb = ctypes.c_void_p(), ctypes.c_size_t()
+            eng._dll.mfx_battle_rollout_buffer(eng.game, name.encode(), 0, ctypes.byref(ptr), ctypes.byref(nb))
+            x = torch.empty(nb.value // torch.tensor([], dtype=dt).element_size(), dtype=dt, device="cuda")
+            eng.rollout_copy(name, x)
+            out.append(x)
+        for g in range(2):
+            for name, w in (("view", 13 * 13 * 7), ("feature", 34)):
+                x = torch.empty(E * rc * w, dtype=torch.float32, device="cuda")
+                eng.rollout_copy(name, x, group=g)
+                out.append(x.view(E, rc, w)[:, :1250].contiguous())
+        return out
+
+    sizes = []
+    for eng in engs:
+        eng.rollout_step(2 * S)                      # two launches: the stale filings are in parity 0
+        eng.rollout_check()
+        n0 = torch.empty(E * 2, dtype=torch.int32, device="cuda")
+        eng.rollout_copy("group_num", n0)
+        acts = torch.empty(E * 2 * rc, dtype=torch.int32, device="cuda")
+        for _ in range(6):                           # per-call steps: the last step's actions again
+            eng.rollout_copy("actions", acts)
+            for g in range(2):
+                eng.set_action(g, acts.view(E, 2, rc)[:, g].contiguous(), rc)
+            eng.step()
+            eng.clear_dead()
+        n1 = torch.empty(E * 2, dtype=torch.int32, device="cuda")
+        eng.rollout_copy("group_num", n1)
+        eng.sync()
+        items = [int(((n + R - 1) // R).sum().item()) for n in (n0, n1)]
+        sizes.append((n0.sum().item(), n1.sum().item(), items[0], items[1]))
+        eng.rollout_step(13)                         # re-seed, then 3 launches
+        eng.rollout_check()
+    assert sizes[0] == sizes[1] and sizes[0][3] < sizes[0][2], sizes       # fewer items to file
+    a, b = dump(engs[0]), dump(engs[1])
+    torch.cuda.synchronize()
+    for k, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8)), k
+
+
 def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
     """The 256x256 bench's own shape (configs[4]: 1024 staggered envs of 2048 + 2048 agents, episode cap
-    400, 8 steps per k_rollout_bigq launch) against the two-stream pipeline at one step per launch,
+    400, 16 steps per k_rollout_bigq launch) against the two-stream pipeline at one step per launch,
     after 408 steps (every env restarts at least once, inside a launch for most): every output
     buffer bit for bit (all rows the first step wrote), the episode statistics, the agent-step
     counters, and no stalled queue."""
@@ -496,11 +549,12 @@ def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
     E, M, N, T = 1024, 256, 2048, 408
     left, right = bd.block_positions(M, N)
     engs = []
-    for fused, sub in (("0", 1), ("1", 8)):
+    for fused, sub in (("0", 1), ("1", 16)):
         monkeypatch.setenv("MFX_BIG_FUSED", fused)
         eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
         eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1234, stagger=True)
         eng.rollout_substeps(sub)
+        assert eng.rollout_path() == ("k_rollout_bigq" if fused == "1" else "k_observe_items+k_rollout_big")
         eng.rollout_step(T)
         engs.append(eng)
     engs[1].rollout_check()
