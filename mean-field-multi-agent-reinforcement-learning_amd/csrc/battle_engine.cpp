@@ -203,6 +203,12 @@ public:
     // fused rollout (bench / throughput path)
     bool rollout_ready = false;
     bool ro_big = false;                     // large envs: k_observe + k_rollout_big, state in HBM
+    bool ro_small_e = false;                 // LDS-sized envs on the large-env path: few envs (small_e_max)
+    // Batches of at most this many LDS-sized envs take the queue kernel (MFX_SMALL_E overrides)
+    static int small_e_max() {
+        const char* v = getenv("MFX_SMALL_E");
+        return v ? atoi(v) : kSmallEMax;
+    }
     RolloutArgs ra{};
     DevBuf<float> ro_view[kMaxGroups], ro_feat[kMaxGroups], ro_rewards, ro_return;
     DevBuf<float> ro_mm;                     // large envs: next observation's minimap   [E][G][169]
@@ -244,6 +250,8 @@ public:
     static constexpr int kBigSplit = 2, kItemGridDiv = 3, kItemRows = 64;
     static constexpr int kBigqRows = 512;         // agents per k_rollout_bigq observation item (64: 9.6e8, 256: 1.06e9, 384-512: 1.08e9, 1024: 1.04e9; profiles/r02_bigq_sweeps.txt)
     static constexpr bool kPipeDefault = false;   // measured slower than the fused step
+    static constexpr int kSmallEMax = 0;          // few-env batches on k_rollout_bigq (measurement pending)
+    static constexpr int kSmallERows = 32;        // agents per item there
     static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
     hipStream_t ro_str[kMaxSplit] = {};
@@ -1077,6 +1085,12 @@ public:
             ro_big = smem > 160 * 1024;
             if (ro_big && (!gp.par_step || big_step_smem_bytes(gp, s.cap, s.acap, true) > 160 * 1024))
                 return fail("rollout: env too large for the fused kernels (%zu bytes of LDS); use the per-call API", smem);
+            // few envs (configs[3]: 8 per GPU): one workgroup per env would leave the chip idle and put each
+            // env's whole observation on one CU; the queue kernel spreads every env's observation over many
+            // workgroups (small items) and steps it in HBM, like the large envs
+            ro_small_e = !ro_big && battle_shape(gp) && n_groups() == 2 && gp.par_step && E <= small_e_max() &&
+                         big_step_smem_bytes(gp, s.cap, s.acap, true) <= 160 * 1024;
+            if (ro_small_e) ro_big = true;
             std::vector<int> hx((size_t)G * tcap, 0), hy((size_t)G * tcap, 0);
             for (int g = 0; g < G; g++)
                 for (int i = 0; i < tmpl_n[g]; i++) { hx[(size_t)g * tcap + i] = xs[g][i]; hy[(size_t)g * tcap + i] = ys[g][i]; }
@@ -1174,7 +1188,7 @@ public:
                     if (ro_item_grid >= kXcds) ro_item_grid -= ro_item_grid % kXcds;   // as many per XCD
                     // the queue-driven kernel: item words hold 13 env bits and 6 chunk bits
                     const char* rv = getenv("MFX_BIGQ_ROWS");                  // sweeps only
-                    const int Rq = rv && atoi(rv) > 0 ? atoi(rv) : kBigqRows;
+                    const int Rq = rv && atoi(rv) > 0 ? atoi(rv) : (ro_small_e ? kSmallERows : kBigqRows);
                     const int chunks = (ra.rowcap + Rq - 1) / Rq;
                     ro_bigq = ro_bigq_want && E <= 8192 && chunks <= 64 && n_groups() == 2 &&
                               bigq_smem_bytes(gp, s.cap, s.acap, Rq) <= 160 * 1024;
@@ -1265,8 +1279,10 @@ public:
                 // clear every slot and move to a fresh tag, so no stale word can pass for an item.
                 ro_qpar = 0;
                 ro_qdone = 0;
+#ifndef MFX_AB_R2_RESEED                 // A/B only: the round-2 re-seed, which the regression test must catch
                 ro_qlaunch++;
                 MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
+#endif
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, 2 * lst * sizeof(int32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
                 MFX_HIP(launch_bigq_seed(d_gp, s, ra, ro_qpar, qtag(ro_qlaunch), ra.step_index, stream));
