@@ -60,10 +60,11 @@ def parse(argv=None):
     # launch ramp-up / tail and the env install / write-back are paid once per 4 steps, +9-11 % over one
     # step per launch; 8 and 16 gain nothing more (profiles/r02_substeps_sweep.txt).  The results are
     # bit-identical for any value (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps).
-    # Large envs (256x256, k_rollout_bigq): 16 steps per launch (the launch's tail is the last envs'
-    # steps): 1.19-1.20e9 against 1.15-1.18e9 at 8 and 1.0-1.07e9 at 4 (profiles/r02_bigq_sweeps.txt).
+    # The queue kernel k_rollout_bigq (256x256 envs, and batches of few 64x64 envs): 16 steps per launch
+    # (the launch's tail is the last envs' steps): 1.19-1.20e9 against 1.15-1.18e9 at 8 and 1.0-1.07e9 at 4
+    # at 256x256 (profiles/r02_bigq_sweeps.txt); 8 envs of 64x64: 0.0435 ms per step vs 0.0472 at 4.
     ap.add_argument("--substeps", type=int, default=None,
-                    help="consecutive steps of every env per launch (default 4 at 64x64, 16 for large maps)")
+                    help="consecutive steps of every env per launch (default 4 on k_rollout, 16 on k_rollout_bigq)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -81,8 +82,6 @@ def parse(argv=None):
         # and the tail of the persistent grid), amortised over more envs: at 4 steps per launch 24576 ->
         # 32768 -> 49152 envs = 1.09 -> 1.137 -> 1.146e9 agent-steps/s (profiles/r02_env_sub_sweep.txt)
         a.envs = 49152 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
-    if a.substeps is None:
-        a.substeps = 4 if a.map * a.map <= 64 * 64 else 16
     return a
 
 
@@ -314,10 +313,10 @@ def main():
     from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing
     eng = BattleBatch(args.map, E, stream=stream)
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
-    S = max(1, args.substeps)
+    path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
+    S = max(1, args.substeps if args.substeps is not None else (16 if path == "k_rollout_bigq" else 4))
     if S != 1:
         eng.rollout_substeps(S)
-    path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
     big = path in ("k_rollout_bigq", "k_observe_items+k_rollout_big")   # large envs, state in HBM
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")

@@ -250,8 +250,12 @@ public:
     static constexpr int kBigSplit = 2, kItemGridDiv = 3, kItemRows = 64;
     static constexpr int kBigqRows = 512;         // agents per k_rollout_bigq observation item (64: 9.6e8, 256: 1.06e9, 384-512: 1.08e9, 1024: 1.04e9; profiles/r02_bigq_sweeps.txt)
     static constexpr bool kPipeDefault = false;   // measured slower than the fused step
-    static constexpr int kSmallEMax = 0;          // few-env batches on k_rollout_bigq (measurement pending)
-    static constexpr int kSmallERows = 32;        // agents per item there
+    // Batches of at most kSmallEMax LDS-sized envs run on k_rollout_bigq (64x64 / 256 agents, one MI355X,
+    // profiles/r03_small_e_sweep.txt, r03_crossover.txt): 8 envs 0.0435 vs 0.0944 ms per step (k_rollout),
+    // 64 envs 0.050 vs 0.121, 1024 envs 3.00e8 vs 2.59e8 agent-steps/s; k_rollout wins from 2048 envs on
+    // (4.0e8 vs 3.2e8).  16-agent items: 0.0435 ms per step at 8 envs vs 0.0461 (32), 0.0497 (64), 0.0441 (8).
+    static constexpr int kSmallEMax = 1024;
+    static constexpr int kSmallERows = 16;
     static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
     hipStream_t ro_str[kMaxSplit] = {};

@@ -1,7 +1,8 @@
 """Summarize rocprofv3 outputs of the bench for profiles/: kernel stats + per-launch HBM bytes.
 
     python scripts/summarize_prof.py <prof_dir> <pmc_fetch_dir> <pmc_write_dir> <envs> <out_json>
-                                     [substeps timed_launches pmc_launches]
+                                     [substeps timed_launches pmc_launches [map bench_json]]
+bench_json (the profiled bench line): adds agent-steps per launch and HBM bytes per agent-step.
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE reads 1/2 of a wide
 coalesced stream (MI355X_MICROARCH.md, HBM) so it is doubled; WRITE_SIZE is exact for 16-B stores.
 Only k_rollout dispatches of the timed part are used (the last `timed_launches` launches of the trace,
@@ -40,5 +41,13 @@ res = {
     "note": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B); last %d k_rollout dispatches of each PMC "
             "pass; %d step(s) of every env per launch" % (npmc, sub),
 }
+if len(sys.argv) > 10:
+    line = json.load(open(sys.argv[10]))
+    units = line["roofline"]["units_per_launch"]
+    res.update({"map": int(sys.argv[9]), "agent_steps_per_launch": units,
+                "hbm_bytes_per_agent_step": res["hbm_bytes_per_launch"] / units,
+                "algorithmic_bytes_per_agent_step": line["roofline"]["bytes_per_unit"],
+                "ratio": res["hbm_bytes_per_launch"] / units / line["roofline"]["bytes_per_unit"],
+                "bench_kernel_ms": line["roofline"]["kernel_ms"], "bench_value": line["value"]})
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -13,12 +13,14 @@ import rollout_check as rck
 pytestmark = pytest.mark.gpu
 
 
-def _run(map_size, n_side, E, T, max_steps, config="battle", VF=13 * 13 * 7, F=34):
+def _run(map_size, n_side, E, T, max_steps, config="battle", VF=13 * 13 * 7, F=34, path=None):
     import torch
     from mfrl_amd.battle import BattleBatch
     left, right = bd.block_positions(map_size, n_side)
     eng = BattleBatch(map_size, E, config=config, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.3, seed=99, stagger=False)
+    if path is not None:
+        assert eng.rollout_path() == path, eng.rollout_path()
     rc = eng.rowcap
     NA = eng.env.get_action_space(eng.handles[0])[0]
     recs = []
@@ -41,12 +43,20 @@ def _run(map_size, n_side, E, T, max_steps, config="battle", VF=13 * 13 * 7, F=3
     return recs, rc
 
 
-@pytest.mark.parametrize("pipe", ["0", "1"])
+PATHS = {"fused": ("0", "0", "k_rollout"), "pipe": ("1", "0", "k_rollout_obs+k_rollout"),
+         "queue": ("0", None, "k_rollout_bigq")}
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("map_size,n_side,E,T,max_steps", [(24, 18, 3, 45, 20), (64, 128, 2, 70, 400)])
-def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps, pipe, monkeypatch):
-    """pipe 0: the fused k_rollout; 1: k_rollout_obs beside k_rollout<.., kSplit> (two state copies)."""
+def test_rollout_matches_oracle(map_size, n_side, E, T, max_steps, path, monkeypatch):
+    """fused: k_rollout; pipe: k_rollout_obs beside k_rollout<.., kSplit> (two state copies); queue: the
+    queue kernel k_rollout_bigq, which takes batches of few LDS-sized envs by default (small_e_max)."""
+    pipe, small_e, want = PATHS[path]
     monkeypatch.setenv("MFX_ROLLOUT_PIPE", pipe)
-    recs, rc = _run(map_size, n_side, E, T, max_steps)
+    if small_e is not None:
+        monkeypatch.setenv("MFX_SMALL_E", small_e)
+    recs, rc = _run(map_size, n_side, E, T, max_steps, path=want)
     left, right = bd.block_positions(map_size, n_side)
     VF, F = 13 * 13 * 7, 34
     for e in range(E):
@@ -182,6 +192,7 @@ def test_rollout_pipe_state_handoff(monkeypatch):
     E, VF, F = 3, 13 * 13 * 7, 34
     left, right = bd.block_positions(64, 128)
     engs = []
+    monkeypatch.setenv("MFX_SMALL_E", "0")           # k_rollout even for 3 envs
     for pipe in ("0", "1"):
         monkeypatch.setenv("MFX_ROLLOUT_PIPE", pipe)
         eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
@@ -327,6 +338,21 @@ def test_rollout_bench_shape_matches_oracle():
     grid, _ = eng.rollout_info()
     assert grid < E                                  # the work queue hands out envs
     _check_launches(eng, 64, 128, _sample_envs(E), T, S, max_steps, seed, 0.2, "k_rollout")
+
+
+@pytest.mark.parametrize("E", [8, 64])
+def test_rollout_small_e_matches_oracle(E):
+    """configs[3]'s per-GPU shape (64 envs over 8 GPUs = 8 per GPU; and 64 on one GPU) as bench.py runs it:
+    64x64 envs on the queue kernel (small_e_max), 16 steps per launch, 416 steps (every env restarts).
+    Every env (E = 8) or 8 sampled envs (E = 64) replayed on the C oracle, compared after every launch."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    T, S, max_steps, seed = 416, 16, 400, 1234
+    left, right = bd.block_positions(64, 128)
+    eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
+    eng.rollout_substeps(S)
+    _check_launches(eng, 64, 128, rck.sample_envs(E, 8), T, S, max_steps, seed, 0.2, "k_rollout_bigq")
 
 
 def test_rollout_bigq_bench_shape_matches_oracle():
