@@ -130,6 +130,12 @@ int mfx_battle_rollout_check(void *game);
 /* The kernels rollout_step runs: 0 k_rollout, 1 k_rollout_obs + k_rollout (pipeline), 2 k_observe_items +
  * k_rollout_big (large-env pipeline), 3 k_rollout_bigq. */
 int mfx_battle_rollout_path(void *game, int *path);
+/* A learned policy in the loop (the fused k_rollout path: batches of LDS-sized envs larger than the few-env
+ * threshold): mode 2 writes every env's observation into the rollout buffers; mode 1 takes the actions in
+ * the rollout's action buffer (a policy forward on that observation, e.g. mfx_qnet_act_rollout), runs
+ * set_action / step / reward / mean action / clear_dead / restart and writes the next observation.  The
+ * mean-action buffer then holds each group's former_act_prob (zeros at an episode's first step). */
+int mfx_battle_rollout_policy_step(void *game, int mode);
 /* Diagnostic build only (libmagent_stamps.so): per-phase s_memtime stamps [E][16]. */
 int mfx_battle_set_stamp_buffer(void *d_buf);
 
@@ -157,6 +163,23 @@ int mfx_mfq_target(const float *d_eq, const float *d_tq, const float *d_r, const
  * default of the python wrapper); 0: NEP-50 (float32), as the same lines run under NumPy 2 */
 int mfx_mfac_returns(float *d_rew, const int64_t *d_offsets, const float *d_value, int n_ep, double gamma,
                      int numpy1, void *stream);
+
+/* ---------------------------------------------------------------- part 5: policy forward */
+/* The Q network of ValueNet._construct_net (algo/base.py:123-183) and its greedy act (:228-254), forward
+ * only, f32 MFMA (csrc/policy_kernels.hip); the Battle view (13 x 13 x 7), features F <= 256, n_action <= 32.
+ * Weights: one float32 blob of n_floats in the layout mfx_qnet_blob_size reports (18 offsets: w1 b1 w2 b2
+ * wd bd we be wp1 bp1 wp2 bp2 w2d b2d wo bo wq bq, every matrix [K][N] row-major, K padded to 4). */
+int mfx_qnet_blob_size(int feature, int n_action, int use_mf, size_t *n_floats, size_t *offsets);
+int mfx_qnet_create(int view_h, int view_w, int n_ch, int feature, int n_action, int use_mf, void **handle);
+int mfx_qnet_destroy(void *handle);
+int mfx_qnet_set_weights(void *handle, const float *d_blob, size_t n_floats, void *stream);
+/* n agents: view [n][1183], feature [n][F], prob [n][A] (mean field, else null) -> q [n][A], act [n] */
+int mfx_qnet_forward(void *handle, const float *d_view, const float *d_feat, const float *d_prob, int n, float *d_q,
+                     int32_t *d_act, void *stream);
+/* group g of a rollout batch -> the rollout's action buffer (live rows); d_rows: E * rowcap + 1 ints scratch */
+int mfx_qnet_act_rollout(void *handle, const float *d_view, const float *d_feat, const int32_t *d_counts,
+                         const double *d_mean, int mean_stride, int E, int G, int g, int rowcap, int32_t *d_rows,
+                         int32_t *d_total, int32_t *d_act, void *stream);
 
 /* ---------------------------------------------------------------- library */
 const char *mfx_last_error(void);

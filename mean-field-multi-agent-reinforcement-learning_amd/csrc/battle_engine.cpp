@@ -1115,6 +1115,7 @@ public:
             ro_mean.ensure((size_t)E * G * na); ro_return.ensure((size_t)E * G); ro_eplen.ensure(E);
             ro_stats.ensure((size_t)E * 4); ro_steps.ensure(E);
             MFX_HIP_THROW(hipMemset(ro_return.p, 0, sizeof(float) * E * G));
+            MFX_HIP_THROW(hipMemset(ro_mean.p, 0, sizeof(double) * ro_mean.n));   // former_act_prob = 0 at step 0
             // stagger episode phases over envs: env e's first episode is cut at max_steps - e*max_steps/E,
             // so after max_steps steps the batch cycles through every phase of an episode uniformly
             std::vector<int32_t> phase((size_t)E);
@@ -1372,6 +1373,31 @@ public:
             cells_stale = true;
             i += k;
         }
+        return 0;
+    }
+
+    // A learned policy's launches (include/magent_amd.h mfx_battle_rollout_policy_step): mode 2 observes every
+    // env into the rollout buffers; mode 1 acts with the actions in the rollout's action buffer (the
+    // policy's forward on that observation), steps, and observes the new state.  The fused k_rollout only.
+    int rollout_policy_step(int mode) {
+        MFX_CHECK(flush_deferred());
+        touch();
+        if (!rollout_ready) return fail("rollout_policy_step before rollout_init");
+        if (mode != 1 && mode != 2) return fail("rollout_policy_step: mode %d (1 step, 2 observe)", mode);
+        if (walls_after_init) return fail("rollout: walls added after rollout_init are not part of the rollout's episodes");
+        {
+            const State& planned = ro_pipe ? ro_pipe_host[ro_par].s : ro_ctx_host.s;
+            if (s.cap != ro_cap || memcmp(&planned, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
+        }
+        if (ro_big || ro_pipe)
+            return fail("rollout_policy_step: a learned policy steps on the fused k_rollout (LDS-sized envs; batches of "
+                        "more than %d envs or MFX_SMALL_E=0; MFX_ROLLOUT_PIPE=0)", small_e_max());
+        MFX_HIP(launch_rollout_mode(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
+                                    ro_grid, mode, stream));
+        ro_launch++;
+        if (mode == 1) ra.step_index++;
+        ra.work_sel ^= 1;
+        cells_stale = true;
         return 0;
     }
 
@@ -2254,6 +2280,10 @@ MFX_API int mfx_battle_rollout_info(void* game, int* grid, int* lds_bytes) {
 // queue reported an error.
 MFX_API int mfx_battle_rollout_check(void* game) {
     MFX_GUARD(MFX_ENV(game)->rollout_check());
+}
+// A learned policy's launches: mode 2 observes every env, mode 1 acts with the action buffer, steps, observes.
+MFX_API int mfx_battle_rollout_policy_step(void* game, int mode) {
+    MFX_GUARD(MFX_ENV(game)->rollout_policy_step(mode));
 }
 // The kernels rollout_step runs: 0 k_rollout, 1 k_rollout_obs + k_rollout (pipeline), 2 k_observe_items +
 // k_rollout_big (large-env pipeline), 3 k_rollout_bigq.

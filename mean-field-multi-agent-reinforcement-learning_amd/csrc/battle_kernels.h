@@ -33,6 +33,9 @@ size_t rollout_smem_bytes(const GameParams& gp, int cells_n, int cap, int acap, 
 hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                           int rows, uint32_t step_index, int work_sel, int qphase, int grid, int split,
                           int n_sub, hipStream_t st);
+hipError_t launch_rollout_mode(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                               int rows, uint32_t step_index, int work_sel, int qphase, int grid, int mode,
+                               hipStream_t st);
 size_t rollout_obs_smem_bytes(const GameParams& gp, int cells_n, int cap, int rows);
 hipError_t launch_rollout_obs(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                               int rows, int work_sel, int qphase, int grid, hipStream_t st);

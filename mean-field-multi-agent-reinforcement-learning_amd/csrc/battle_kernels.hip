@@ -373,6 +373,25 @@ hipError_t launch_rollout(const GameParams& gp, const GameParams* d_gp, const St
     });
 }
 
+// A learned policy's launches (k_rollout kMode 1: act with ra.actions, step, observe; 2: observe only),
+// one step each; the fused path only (LDS-sized envs, no pipeline).
+hipError_t launch_rollout_mode(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
+                               int rows, uint32_t step_index, int work_sel, int qphase, int grid, int mode,
+                               hipStream_t st) {
+    const size_t smem = rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, rows);
+    if (smem > 160 * 1024 || (mode != 1 && mode != 2)) return hipErrorInvalidValue;
+    auto go = [&](auto kern) {
+        kern<<<grid, MFX_ROLLOUT_THREADS, smem, st>>>(d_gp, d_ctx, step_index, work_sel, qphase, 1);
+        return hipGetLastError();
+    };
+    if (is_battle_shape(gp)) {
+        if (rollout_prefetch_ok(gp, s))
+            return mode == 1 ? go(k_rollout<true, true, false, 1>) : go(k_rollout<true, true, false, 2>);
+        return mode == 1 ? go(k_rollout<true, false, false, 1>) : go(k_rollout<true, false, false, 2>);
+    }
+    return mode == 1 ? go(k_rollout<false, false, false, 1>) : go(k_rollout<false, false, false, 2>);
+}
+
 // k_rollout_obs: the env image and the observation scratch
 size_t rollout_obs_smem_bytes(const GameParams& gp, int cells_n, int cap, int rows) {
     const bool kB = is_battle_shape(gp);

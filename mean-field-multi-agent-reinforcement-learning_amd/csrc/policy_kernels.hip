@@ -1,0 +1,460 @@
+// policy_kernels.hip -- the reference's Q network (ValueNet._construct_net, algo/base.py:123-183) and its
+// greedy act (ValueNet.act, :228-254), forward only, hand-written for gfx950 on the f32-input MFMA
+// v_mfma_f32_16x16x4_f32 (exact f32: each product rounded once into an f32 accumulator, the rate of the
+// f32 VALU -- MI355X_MICROARCH.md; there is no xf32 / TF32 on gfx950).  The network, per agent:
+//
+//   view [13][13][7] --Conv1 3x3x32 valid, relu--> [11][11][32] --Conv2 3x3x32 valid, relu--> [9][9][32]
+//   flatten (TF's NHWC order, 2,592) --Dense-Obs 256, relu--> h_obs
+//   feature [F] --Dense-Emb 32, relu--> h_emb
+//   (mean field) prob [A] --Prob-Emb 64, relu--> --Dense-Act-Prob 32, relu--> h_prob
+//   concat(h_obs, h_emb[, h_prob]) --Dense2 128, relu--> --Dense-Out 64, relu--> --Q-Value A--> q
+//   act = argmax q   (the reference takes argmax of softmax(q / T), the same index up to float ties)
+//
+// 3.4 MFLOP per agent (conv2 44 %, Dense-Obs 39 %, conv1 14 %): compute-bound at the f32 matrix rate
+// (157 TF/s -> ~4.6e7 agents/s for the whole chip).  Two kernels:
+//   k_qnet_conv  one wave per agent: the view staged in LDS, Conv1 as an implicit GEMM over 121
+//                positions x 32 channels x K 63 (padded to 64), its output kept in LDS, Conv2 as an
+//                implicit GEMM over 81 positions x 32 x K 288; the 2,592 activations to HBM (10 KB/agent)
+//   k_qnet_head  four waves x 16 agents per workgroup: Dense-Obs as a GEMM (K 2,592) with the weight
+//                chunks staged once per workgroup in LDS and shared by the four waves, then the small
+//                layers the same way, the Q values and the argmax
+// A and B operands of v_mfma_f32_16x16x4_f32: lane l holds A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15];
+// D: lane l holds D[(l >> 4) * 4 + r][l & 15], r = 0..3 (cdna_hip_programming.md, fragment layout).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "mfx_common.h"
+#include "../../include/magent_amd.h"
+
+namespace mfx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kQVH = 13, kQVW = 13, kQNC = 7;           // Battle view (13 x 13 x 7)
+constexpr int kQViewF = kQVH * kQVW * kQNC;             // 1,183
+constexpr int kQC1 = 11, kQC2 = 9, kQCh = 32;            // conv output sides, channels
+constexpr int kQK1 = 64;                                 // conv1 K: 3 * 3 * 7 = 63, padded
+constexpr int kQK2 = 3 * 3 * kQCh;                       // conv2 K: 288
+constexpr int kQFlat = kQC2 * kQC2 * kQCh;               // 2,592
+constexpr int kQHObs = 256, kQHEmb = 32, kQHP1 = 64, kQHP2 = 32, kQH2 = 128, kQHOut = 64, kQMaxA = 32;
+constexpr int kQActW = kQHObs + kQHEmb + kQHP2;          // concat width, mean field (288 without)
+constexpr int kQActLd = kQActW + 4;                      // LDS row stride of the activations (bank spread)
+
+// Device view of one packed weight blob (layout: QNetLayout; every matrix [K][N] row-major, K padded to a
+// multiple of 4 with zero rows, N of the Q layer padded to 32 with zero columns).
+struct QNetDev {
+    const float *w1, *b1, *w2, *b2, *wd, *bd, *we, *be, *wp1, *bp1, *wp2, *bp2, *w2d, *b2d, *wo, *bo, *wq, *bq;
+    int F, Fp, A, Ap, use_mf, Kc;   // Kc: Dense2 input width (288, or 320 with mean field)
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void qwave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------------------------------ conv
+// LDS: w1 [64][32], w2 [288][32] (shared), per wave the view [1,184] and conv1's output [121][32].
+constexpr int kQConvWaves = 4;
+constexpr int kQViewLds = 1184, kQC1Lds = kQC1 * kQC1 * kQCh;
+constexpr size_t kQConvSmem = (size_t)(kQK1 * kQCh + kQK2 * kQCh + kQConvWaves * (kQViewLds + kQC1Lds)) * 4;
+
+// Offset of im2col column k (ky, kx, ci) in the staged 13 x 13 x 7 view; the pad column 63 reads
+// element 0 against a zero weight row.
+__device__ __forceinline__ int conv1_koff(int k) {
+    if (k >= 63) return 0;
+    const int ky = k / 21, kx = (k % 21) / 7, ci = k % 7;
+    return (ky * kQVW + kx) * kQNC + ci;
+}
+
+// rows: view row of compact agent i (null: i); view_ld: floats per view row.  out: [n][2,592].
+__global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __restrict__ view, size_t view_ld,
+                                                      const int32_t* __restrict__ rows, int n, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float qsm[];
+    float* w1 = qsm;
+    float* w2 = w1 + kQK1 * kQCh;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
+    float* vs = w2 + kQK2 * kQCh + wid * (kQViewLds + kQC1Lds);
+    float* c1 = vs + kQViewLds;
+    for (int i = threadIdx.x; i < kQK1 * kQCh; i += blockDim.x) w1[i] = p.w1[i];
+    for (int i = threadIdx.x; i < kQK2 * kQCh; i += blockDim.x) w2[i] = p.w2[i];
+    __syncthreads();
+    // conv1's B operands for all 16 k-steps stay in registers, so do the lane's im2col offsets
+    float b1r[16][2];
+    int koff[16];
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+        b1r[kk][0] = w1[(kk * 4 + h) * kQCh + c];
+        b1r[kk][1] = w1[(kk * 4 + h) * kQCh + 16 + c];
+        koff[kk] = conv1_koff(kk * 4 + h);
+    }
+    const float bias1a = p.b1[c], bias1b = p.b1[16 + c], bias2a = p.b2[c], bias2b = p.b2[16 + c];
+    for (int i = blockIdx.x * kQConvWaves + wid; i < n; i += gridDim.x * kQConvWaves) {
+        const float* src = view + (size_t)(rows ? rows[i] : i) * view_ld;
+        for (int q = lane; q < kQViewF; q += 64) vs[q] = src[q];
+        qwave_sync();
+        // ---- Conv1: 8 position tiles (121 of 128 rows) x 2 channel tiles, K 64
+        for (int mt = 0; mt < 8; ++mt) {
+            const int pa = min(mt * 16 + c, kQC1 * kQC1 - 1);
+            const int vb = ((pa / kQC1) * kQVW + pa % kQC1) * kQNC;
+            f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const float a = vs[vb + koff[kk]];
+                d0 = mfma4(a, b1r[kk][0], d0);
+                d1 = mfma4(a, b1r[kk][1], d1);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int pos = mt * 16 + h * 4 + r;
+                if (pos < kQC1 * kQC1) {
+                    c1[pos * kQCh + c] = fmaxf(d0[r] + bias1a, 0.f);
+                    c1[pos * kQCh + 16 + c] = fmaxf(d1[r] + bias1b, 0.f);
+                }
+            }
+        }
+        qwave_sync();
+        // ---- Conv2: 6 position tiles (81 of 96 rows) x 2 channel tiles, K 288 (72 k-steps); im2col
+        // column k = 4 kk + h is (ky, kx, ci) = (kk / 24, kk / 8 % 3, 4 (kk % 8) + h)
+        f32x4 acc[6][2];
+        int cb[6];
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt) {
+            const int pa = min(mt * 16 + c, kQC2 * kQC2 - 1);
+            cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQCh + h;
+            acc[mt][0] = {0.f, 0.f, 0.f, 0.f};
+            acc[mt][1] = {0.f, 0.f, 0.f, 0.f};
+        }
+        for (int kk = 0; kk < kQK2 / 4; ++kk) {
+            const int so = ((kk / 24) * kQC1 + (kk / 8) % 3) * kQCh + (kk % 8) * 4;
+            const float b0 = w2[(kk * 4 + h) * kQCh + c], b1 = w2[(kk * 4 + h) * kQCh + 16 + c];
+#pragma unroll
+            for (int mt = 0; mt < 6; ++mt) {
+                const float a = c1[cb[mt] + so];
+                acc[mt][0] = mfma4(a, b0, acc[mt][0]);
+                acc[mt][1] = mfma4(a, b1, acc[mt][1]);
+            }
+        }
+        float* o = out + (size_t)i * kQFlat;
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int pos = mt * 16 + h * 4 + r;
+                if (pos < kQC2 * kQC2) {
+                    o[pos * kQCh + c] = fmaxf(acc[mt][0][r] + bias2a, 0.f);
+                    o[pos * kQCh + 16 + c] = fmaxf(acc[mt][1][r] + bias2b, 0.f);
+                }
+            }
+        qwave_sync();                                    // vs / c1 are rewritten by the next agent
+    }
+}
+
+// ------------------------------------------------------------------------------------------ head
+// One workgroup = 4 waves x 16 agents.  wg_gemm: every wave multiplies ITS 16 rows of A (a functor of
+// the k-step) by the same B [K][NT * 16], whose 16-row chunks the whole workgroup stages in LDS (double
+// buffered), accumulating into acc[NT].  Call sites are uniform across the workgroup (barriers inside).
+constexpr int kQHeadWaves = 4, kQKC = 16;                // agents per wave = 16; B rows per chunk
+constexpr int kQBLd = kQHObs + 16;                       // LDS stride of a B chunk row (bank spread)
+constexpr size_t kQHeadSmem = (size_t)(2 * kQKC * kQBLd + kQHeadWaves * 16 * kQActLd + kQHeadWaves * 16 * kQHP1) * 4;
+
+template <int NT, class AF>
+__device__ __forceinline__ void wg_gemm(const float* __restrict__ B, int K, AF a_at, float* bsm, f32x4* acc) {
+    constexpr int N = NT * 16;
+    const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
+    const int nchunk = (K + kQKC - 1) / kQKC;
+    auto stage = [&](int ch, float* dst) {               // rows [ch * 16, +16) of B (zero past K)
+        for (int q = threadIdx.x; q < kQKC * N; q += blockDim.x) {
+            const int r = q / N, col = q - r * N, k = ch * kQKC + r;
+            dst[r * kQBLd + col] = k < K ? B[(size_t)k * N + col] : 0.f;
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+    stage(0, bsm);
+    __syncthreads();
+    for (int ch = 0; ch < nchunk; ++ch) {
+        float* cur = bsm + (ch & 1) * kQKC * kQBLd;
+        if (ch + 1 < nchunk) stage(ch + 1, bsm + ((ch + 1) & 1) * kQKC * kQBLd);
+#pragma unroll
+        for (int s = 0; s < kQKC / 4; ++s) {
+            const int kk = ch * (kQKC / 4) + s;
+            if (kk * 4 >= K) break;
+            const float a = a_at(kk);
+            const float* brow = cur + (s * 4 + h) * kQBLd + c;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma4(a, brow[t * 16], acc[t]);
+        }
+        __syncthreads();
+    }
+}
+
+// Write relu(acc + bias) of NT tiles into this wave's activation rows at column col0.
+template <int NT>
+__device__ __forceinline__ void put_relu(const f32x4* acc, const float* __restrict__ bias, float* act, int ld, int col0) {
+    const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const float b = bias[t * 16 + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[(h * 4 + r) * ld + col0 + t * 16 + c] = fmaxf(acc[t][r] + b, 0.f);
+    }
+}
+
+// Compact agent i -> (view row, action slot, prob row): rows == null: (i, i, i); else row = rows[i]
+// = e * rowcap + j of a rollout buffer, action slot e * act_env + act_off + j, prob row e.
+struct QRowMap {
+    const int32_t* rows;
+    int rowcap, act_env, act_off;
+};
+
+template <typename PT>
+__global__ void __launch_bounds__(256, 1) k_qnet_head(QNetDev p, const float* __restrict__ conv, int n,
+                                                      const float* __restrict__ feat, size_t feat_ld,
+                                                      const PT* __restrict__ prob, size_t prob_ld, QRowMap rm,
+                                                      float* __restrict__ q_out, int32_t* __restrict__ act_out) {
+    extern __shared__ __attribute__((aligned(16))) float qsm[];
+    float* bsm = qsm;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
+    float* act = bsm + 2 * kQKC * kQBLd + wid * 16 * kQActLd;            // [16][kQActLd]
+    float* tmp = bsm + 2 * kQKC * kQBLd + kQHeadWaves * 16 * kQActLd + wid * 16 * kQHP1;   // [16][64]
+    const int base = (blockIdx.x * kQHeadWaves + wid) * 16;
+    const int ia = min(base + c, n - 1);                 // this lane's A row (clamped: junk rows, never written)
+    const int row = rm.rows ? rm.rows[ia] : ia;
+    const int env = rm.rows ? row / rm.rowcap : ia;
+    f32x4 acc[16];
+    // ---- Dense-Obs: [16 x 2592] x [2592 x 256]
+    {
+        const float* ar = conv + (size_t)ia * kQFlat + h;
+        wg_gemm<16>(p.wd, kQFlat, [&](int kk) { return ar[kk * 4]; }, bsm, acc);
+        put_relu<16>(acc, p.bd, act, kQActLd, 0);
+    }
+    // ---- Dense-Emb: [16 x F] x [F x 32]
+    {
+        const float* fr = feat + (size_t)row * feat_ld;
+        const int F = p.F;
+        wg_gemm<2>(p.we, p.Fp, [&](int kk) { const int k = kk * 4 + h; return k < F ? fr[k] : 0.f; }, bsm, acc);
+        put_relu<2>(acc, p.be, act, kQActLd, kQHObs);
+    }
+    // ---- mean field: Prob-Emb 64, Dense-Act-Prob 32 (the prob input cast to float32 as the placeholder does)
+    if (p.use_mf) {
+        const PT* pr = prob + (size_t)env * prob_ld;
+        const int A = p.A;
+        wg_gemm<4>(p.wp1, p.Ap, [&](int kk) { const int k = kk * 4 + h; return k < A ? (float)pr[k] : 0.f; }, bsm, acc);
+        put_relu<4>(acc, p.bp1, tmp, kQHP1, 0);
+        qwave_sync();
+        wg_gemm<2>(p.wp2, kQHP1, [&](int kk) { return tmp[c * kQHP1 + kk * 4 + h]; }, bsm, acc);
+        put_relu<2>(acc, p.bp2, act, kQActLd, kQHObs + kQHEmb);
+    }
+    qwave_sync();
+    // ---- Dense2 128, Dense-Out 64 (tmp), Q-Value
+    wg_gemm<8>(p.w2d, p.Kc, [&](int kk) { return act[c * kQActLd + kk * 4 + h]; }, bsm, acc);
+    qwave_sync();
+    put_relu<8>(acc, p.b2d, act, kQActLd, 0);           // (the concat row is consumed: reuse it)
+    qwave_sync();
+    wg_gemm<4>(p.wo, kQH2, [&](int kk) { return act[c * kQActLd + kk * 4 + h]; }, bsm, acc);
+    put_relu<4>(acc, p.bo, tmp, kQHP1, 0);
+    qwave_sync();
+    wg_gemm<2>(p.wq, kQHOut, [&](int kk) { return tmp[c * kQHP1 + kk * 4 + h]; }, bsm, acc);
+    // Q values to LDS (reusing act), then one lane per agent: output and argmax (first maximum)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const float b = p.bq[t * 16 + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[(h * 4 + r) * kQActLd + t * 16 + c] = acc[t][r] + b;
+    }
+    qwave_sync();
+    if (lane < 16 && base + lane < n) {
+        const int i = base + lane;
+        const float* qr = act + lane * kQActLd;
+        int best = 0;
+        float bv = qr[0];
+        for (int k = 0; k < p.A; ++k) {
+            const float x = qr[k];
+            if (q_out) q_out[(size_t)i * p.A + k] = x;
+            if (x > bv) { bv = x; best = k; }
+        }
+        if (act_out) {
+            const int r = rm.rows ? rm.rows[i] : i;
+            const size_t slot = rm.rows ? (size_t)(r / rm.rowcap) * rm.act_env + rm.act_off + r % rm.rowcap : (size_t)i;
+            act_out[slot] = best;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------ rollout rows
+// The compact row list of one group of a rollout batch: rows e * rowcap + j for j < n_e (n_e = the group's
+// size in the [E][G] counts), in env order.  One workgroup: a scan over E counts.
+__global__ void __launch_bounds__(1024) k_qnet_rows(const int32_t* __restrict__ counts, int E, int G, int g, int rowcap,
+                                                    int32_t* __restrict__ rows, int32_t* __restrict__ total) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x, per = (E + 1023) / 1024;
+    const int e0 = min(E, t * per), e1 = min(E, e0 + per);
+    int s = 0;
+    for (int e = e0; e < e1; ++e) s += min(counts[e * G + g], rowcap);
+    part[t] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {                 // inclusive scan (Hillis-Steele)
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int off = part[t] - s;
+    for (int e = e0; e < e1; ++e) {
+        const int m = min(counts[e * G + g], rowcap);
+        for (int j = 0; j < m; ++j) rows[off + j] = e * rowcap + j;
+        off += m;
+    }
+    if (t == 1023) *total = part[1023];
+}
+
+}  // namespace mfx
+
+// ------------------------------------------------------------------------------------------ C ABI
+using namespace mfx;
+
+namespace {
+struct QNetHandle {
+    QNetDev dev{};
+    float* blob = nullptr;
+    size_t blob_n = 0;
+    DevBuf<float> conv;           // [n][2592] activations between the kernels
+};
+
+// Offsets (floats) of every matrix / bias in the packed blob, in the order of QNetDev.
+void qnet_layout(int F, int A, int use_mf, size_t* off, size_t* total, int* Fp, int* Ap, int* Kc) {
+    *Fp = (F + 3) & ~3;
+    *Ap = (A + 3) & ~3;
+    *Kc = kQHObs + kQHEmb + (use_mf ? kQHP2 : 0);
+    const size_t sizes[18] = {(size_t)kQK1 * kQCh, kQCh, (size_t)kQK2 * kQCh, kQCh, (size_t)kQFlat * kQHObs, kQHObs,
+                              (size_t)*Fp * kQHEmb, kQHEmb, (size_t)*Ap * kQHP1, kQHP1, (size_t)kQHP1 * kQHP2, kQHP2,
+                              (size_t)*Kc * kQH2, kQH2, (size_t)kQH2 * kQHOut, kQHOut, (size_t)kQHOut * kQMaxA, kQMaxA};
+    size_t o = 0;
+    for (int k = 0; k < 18; ++k) { off[k] = o; o += (sizes[k] + 3) & ~(size_t)3; }
+    *total = o;
+}
+}  // namespace
+
+extern "C" {
+
+MFX_API int mfx_qnet_blob_size(int feature, int n_action, int use_mf, size_t* n_floats, size_t* offsets) {
+    if (feature < 1 || feature > 256 || n_action < 1 || n_action > kQMaxA) return fail("qnet: feature 1..256, n_action 1..32");
+    size_t off[18];
+    int Fp, Ap, Kc;
+    qnet_layout(feature, n_action, use_mf, off, n_floats, &Fp, &Ap, &Kc);
+    if (offsets) for (int k = 0; k < 18; ++k) offsets[k] = off[k];
+    return 0;
+}
+
+MFX_API int mfx_qnet_create(int view_h, int view_w, int n_ch, int feature, int n_action, int use_mf, void** handle) {
+    if (view_h != kQVH || view_w != kQVW || n_ch != kQNC)
+        return fail("qnet: the HIP forward takes the Battle view (13 x 13 x 7); got %d x %d x %d", view_h, view_w, n_ch);
+    size_t n = 0;
+    MFX_CHECK(mfx_qnet_blob_size(feature, n_action, use_mf, &n, nullptr));
+    auto* q = new QNetHandle();
+    if (hipMalloc(&q->blob, n * sizeof(float)) != hipSuccess) { delete q; return fail("qnet: hipMalloc of %zu floats", n); }
+    q->blob_n = n;
+    size_t off[18];
+    size_t tot;
+    int Fp, Ap, Kc;
+    qnet_layout(feature, n_action, use_mf, off, &tot, &Fp, &Ap, &Kc);
+    const float** f[18] = {&q->dev.w1, &q->dev.b1, &q->dev.w2, &q->dev.b2, &q->dev.wd, &q->dev.bd, &q->dev.we, &q->dev.be,
+                           &q->dev.wp1, &q->dev.bp1, &q->dev.wp2, &q->dev.bp2, &q->dev.w2d, &q->dev.b2d, &q->dev.wo,
+                           &q->dev.bo, &q->dev.wq, &q->dev.bq};
+    for (int k = 0; k < 18; ++k) *f[k] = q->blob + off[k];
+    q->dev.F = feature; q->dev.Fp = Fp; q->dev.A = n_action; q->dev.Ap = Ap; q->dev.use_mf = use_mf; q->dev.Kc = Kc;
+    *handle = q;
+    return 0;
+}
+
+MFX_API int mfx_qnet_destroy(void* handle) {
+    auto* q = static_cast<QNetHandle*>(handle);
+    if (!q) return 0;
+    if (q->blob) (void)hipFree(q->blob);
+    delete q;
+    return 0;
+}
+
+// d_blob: n_floats packed by the caller (mfx_qnet_blob_size offsets), copied on `stream`.
+MFX_API int mfx_qnet_set_weights(void* handle, const float* d_blob, size_t n_floats, void* stream) {
+    auto* q = static_cast<QNetHandle*>(handle);
+    if (n_floats != q->blob_n) return fail("qnet_set_weights: %zu floats, the layout has %zu", n_floats, q->blob_n);
+    MFX_HIP(hipMemcpyAsync(q->blob, d_blob, n_floats * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+// Agents per conv -> head pass: the Conv2 activations of a pass sit in HBM between the two kernels
+// (10 KB per agent: 2.7 GB at this size).
+constexpr int kQPass = 1 << 18;
+
+static int qnet_run(QNetHandle* q, const float* view, size_t view_ld, const float* feat, size_t feat_ld,
+                    const void* prob, int prob_f64, size_t prob_ld, QRowMap rm, int n, float* q_out, int32_t* act,
+                    hipStream_t st) {
+    if (n <= 0) return 0;
+    if (q->dev.use_mf && !prob) return fail("qnet: the mean-field net needs prob");
+    try { q->conv.ensure((size_t)std::min(n, kQPass) * kQFlat); } catch (const HipFailure& f) { return fail("%s", f.what()); }
+    int dev = 0, cus = 0;
+    MFX_HIP(hipGetDevice(&dev));
+    MFX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    for (int off = 0; off < n; off += kQPass) {
+        const int m = std::min(kQPass, n - off);
+        QRowMap r = rm;
+        if (r.rows) r.rows += off;
+        // dense rows: pass `off` shifts every row-indexed input / output
+        const float* v = r.rows ? view : view + (size_t)off * view_ld;
+        const float* f = r.rows ? feat : feat + (size_t)off * feat_ld;
+        const void* pb = prob;
+        if (prob && !r.rows) pb = prob_f64 ? (const void*)(static_cast<const double*>(prob) + (size_t)off * prob_ld)
+                                           : (const void*)(static_cast<const float*>(prob) + (size_t)off * prob_ld);
+        float* qo = q_out ? q_out + (size_t)off * q->dev.A : nullptr;
+        int32_t* ao = act ? (r.rows ? act : act + off) : nullptr;
+        const int cgrid = std::min((m + kQConvWaves - 1) / kQConvWaves, cus * 8);
+        k_qnet_conv<<<cgrid, 256, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p);
+        MFX_HIP(hipGetLastError());
+        const int hgrid = (m + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
+        if (prob_f64)
+            k_qnet_head<double><<<hgrid, 256, kQHeadSmem, st>>>(q->dev, q->conv.p, m, f, feat_ld,
+                                                                 static_cast<const double*>(pb), prob_ld, r, qo, ao);
+        else
+            k_qnet_head<float><<<hgrid, 256, kQHeadSmem, st>>>(q->dev, q->conv.p, m, f, feat_ld,
+                                                                static_cast<const float*>(pb), prob_ld, r, qo, ao);
+        MFX_HIP(hipGetLastError());
+    }
+    return 0;
+}
+
+// n agents, dense rows: view [n][1183], feature [n][F], prob [n][A] float32 (mean field; else null).
+// q_out [n][A] and act [n] (either may be null).
+MFX_API int mfx_qnet_forward(void* handle, const float* d_view, const float* d_feat, const float* d_prob, int n,
+                             float* d_q, int32_t* d_act, void* stream) {
+    auto* q = static_cast<QNetHandle*>(handle);
+    QRowMap rm{nullptr, 1, 0, 0};
+    return qnet_run(q, d_view, kQViewF, d_feat, q->dev.F, d_prob, 0, q->dev.A, rm, n, d_q, d_act, (hipStream_t)stream);
+}
+
+// Group g of a rollout batch ([E][rowcap] view / feature rows, counts [E][G], former mean actions
+// [E][G][mean_stride] float64): actions into d_act [E][G][rowcap] for the group's live rows.  d_rows:
+// scratch of E * rowcap ints, d_total: one int.  The row list is built on the device; n_max bounds the
+// rows the kernels are launched for (E * rowcap).
+MFX_API int mfx_qnet_act_rollout(void* handle, const float* d_view, const float* d_feat, const int32_t* d_counts,
+                                 const double* d_mean, int mean_stride, int E, int G, int g, int rowcap,
+                                 int32_t* d_rows, int32_t* d_total, int32_t* d_act, void* stream) {
+    auto* q = static_cast<QNetHandle*>(handle);
+    hipStream_t st = (hipStream_t)stream;
+    k_qnet_rows<<<1, 1024, 0, st>>>(d_counts, E, G, g, rowcap, d_rows, d_total);
+    MFX_HIP(hipGetLastError());
+    int total = 0;
+    MFX_HIP(hipMemcpyAsync(&total, d_total, sizeof(int), hipMemcpyDeviceToHost, st));
+    MFX_HIP(hipStreamSynchronize(st));
+    QRowMap rm{d_rows, rowcap, G * rowcap, g * rowcap};
+    return qnet_run(q, d_view, kQViewF, d_feat, q->dev.F, d_mean + (size_t)g * mean_stride, 1, (size_t)G * mean_stride,
+                    rm, total, nullptr, d_act, st);
+}
+
+}  // extern "C"

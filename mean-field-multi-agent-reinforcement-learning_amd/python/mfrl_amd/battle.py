@@ -32,7 +32,8 @@ class BattleBatch:
                    "mfx_battle_sync", "mfx_battle_rollout_init", "mfx_battle_rollout_step",
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
-                   "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check", "mfx_battle_rollout_path"):
+                   "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check", "mfx_battle_rollout_path",
+                   "mfx_battle_rollout_policy_step"):
             try:
                 getattr(self._dll, fn).restype = ctypes.c_int
             except AttributeError:          # an older build of the library (A/B runs)
@@ -53,6 +54,11 @@ class BattleBatch:
         """stream: a torch.cuda.Stream (or a raw hipStream_t as int)."""
         raw = getattr(stream, "cuda_stream", stream)
         self._check(self._dll.mfx_battle_set_stream(self.game, ctypes.c_void_p(raw)), "set_stream")
+        self._stream_raw = raw
+
+    def stream_handle(self):
+        """The hipStream_t the engine launches on (0: the null stream)."""
+        return getattr(self, "_stream_raw", 0) or 0
 
     # ------------------------------------------------------------------ reference call sequence
     def reset(self):
@@ -134,6 +140,23 @@ class BattleBatch:
 
     def rollout_step(self, n_steps=1):
         self._check(self._dll.mfx_battle_rollout_step(self.game, n_steps), "rollout_step")
+
+    # ------------------------------------------------------------------ learned policy in the loop
+    def rollout_policy_observe(self):
+        """Write every env's observation into the rollout buffers (the first step of a learned-policy loop)."""
+        self._check(self._dll.mfx_battle_rollout_policy_step(self.game, 2), "rollout_policy_step")
+
+    def rollout_policy_step(self):
+        """Act with the rollout's action buffer (a policy's forward on the current observation, e.g.
+        mfrl_amd.policy.QNetHIP.act_rollout), step every env, observe the new state."""
+        self._check(self._dll.mfx_battle_rollout_policy_step(self.game, 1), "rollout_policy_step")
+
+    def mean_stride(self):
+        """Doubles per [env][group] row of the mean-action buffer (the largest n_action)."""
+        p, nb = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self._dll.mfx_battle_rollout_buffer(self.game, b"mean_action", 0, ctypes.byref(p),
+                                                        ctypes.byref(nb)), "rollout_buffer")
+        return nb.value // 8 // (self.n_envs * len(self.handles))
 
     def rollout_copy(self, name, dst, group=0, nbytes=None):
         """Copy a device rollout buffer into dst (numpy array or torch tensor, host or device)."""

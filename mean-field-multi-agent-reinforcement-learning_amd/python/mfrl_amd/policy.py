@@ -1,0 +1,153 @@
+"""QNetHIP: the hand-written HIP forward (csrc/policy_kernels.hip) of the reference's Q network.
+
+    ValueNet._construct_net  examples/battle_model/algo/base.py:123-183   -> QNetHIP.forward (q values)
+    ValueNet.act             examples/battle_model/algo/base.py:228-254   -> QNetHIP.act (argmax q)
+
+The weights come from a torch QNet (mfrl_amd.algo.nets, the layer-for-layer port that training updates):
+``load(qnet)`` packs them into the device layout the kernels read -- every matrix [K][N] row-major with
+the im2col / NHWC-flatten orders of TF (conv kernels [ky][kx][ci][co], Dense-Obs rows in (y, x, c) order),
+K padded to a multiple of 4 with zero rows -- and uploads them in one copy.  Forward only: training keeps
+the torch module (autograd); after an optimiser step call ``load`` again.
+
+Numerics: f32 inputs and weights, f32 MFMA accumulation (one rounding per product); the result differs
+from the torch module's by summation order only (|dq| ~1e-6 at these sizes, tests/test_policy_gpu.py).
+"""
+import ctypes
+
+import torch
+
+from . import check, lib
+
+_P = ctypes.c_void_p
+
+
+def _ptr(t):
+    return _P(t.data_ptr()) if t is not None else _P()
+
+
+def _stream():
+    return _P(torch.cuda.current_stream().cuda_stream)
+
+
+N_BLOCKS = 18      # w1 b1 w2 b2 wd bd we be wp1 bp1 wp2 bp2 w2d b2d wo bo wq bq (policy_kernels.hip)
+
+
+def blob_layout(feature, n_action, use_mf):
+    """(floats in the packed blob, the 18 block offsets) -- mfx_qnet_blob_size (host only, no GPU)."""
+    L = lib()
+    L.mfx_qnet_blob_size.restype = ctypes.c_int
+    n = ctypes.c_size_t()
+    off = (ctypes.c_size_t * N_BLOCKS)()
+    check(L.mfx_qnet_blob_size(int(feature), int(n_action), int(bool(use_mf)), ctypes.byref(n), off),
+          "mfx_qnet_blob_size")
+    return n.value, list(off)
+
+
+def pack_qnet(net, feature, n_action, use_mf, layout=None):
+    """The device-layout blob (float32, on net's device) of a torch QNet (mfrl_amd.algo.nets.QNet)."""
+    F, A, mf = int(feature), int(n_action), bool(use_mf)
+    n, offsets = layout or blob_layout(F, A, mf)
+    Fp, Ap = (F + 3) & ~3, (A + 3) & ~3
+    dev = net.conv1.weight.device
+    blob = torch.zeros(n, dtype=torch.float32, device=dev)
+
+    def put(k, mat, rows=None, cols=None):
+        m = mat.detach().to(torch.float32)
+        if m.dim() == 1:
+            blob[offsets[k]:offsets[k] + m.numel()] = m
+            return
+        R, C = m.shape
+        R2, C2 = rows or R, cols or C
+        full = torch.zeros((R2, C2), dtype=torch.float32, device=dev)
+        full[:R, :C] = m
+        blob[offsets[k]:offsets[k] + R2 * C2] = full.reshape(-1)
+
+    put(0, net.conv1.weight.permute(2, 3, 1, 0).reshape(-1, 32), rows=64)       # [ky][kx][ci][co]
+    put(1, net.conv1.bias)
+    put(2, net.conv2.weight.permute(2, 3, 1, 0).reshape(-1, 32))
+    put(3, net.conv2.bias)
+    put(4, net.dense_obs.weight.t())                                          # [2592 (y, x, c)][256]
+    put(5, net.dense_obs.bias)
+    put(6, net.dense_emb.weight.t(), rows=Fp)
+    put(7, net.dense_emb.bias)
+    if mf:
+        put(8, net.prob_emb.weight.t(), rows=Ap)
+        put(9, net.prob_emb.bias)
+        put(10, net.dense_act_prob.weight.t())
+        put(11, net.dense_act_prob.bias)
+    put(12, net.dense2.weight.t())
+    put(13, net.dense2.bias)
+    put(14, net.dense_out.weight.t())
+    put(15, net.dense_out.bias)
+    put(16, net.q_value.weight.t(), cols=32)                                  # Q columns padded to 32
+    put(17, net.q_value.bias)
+    return blob
+
+
+class QNetHIP:
+    def __init__(self, view_space, feature_space, num_actions, use_mf=False):
+        h, w, c = view_space
+        self.F, self.A, self.use_mf = int(feature_space[0]), int(num_actions), bool(use_mf)
+        L = lib()
+        for fn in ("mfx_qnet_create", "mfx_qnet_destroy", "mfx_qnet_set_weights", "mfx_qnet_forward",
+                   "mfx_qnet_act_rollout"):
+            getattr(L, fn).restype = ctypes.c_int
+        self._L = L
+        self.blob_n, self.offsets = blob_layout(self.F, self.A, self.use_mf)
+        hdl = _P()
+        check(L.mfx_qnet_create(int(h), int(w), int(c), self.F, self.A, int(self.use_mf), ctypes.byref(hdl)),
+              "mfx_qnet_create")
+        self.handle = hdl
+        self._rows = None
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self._L.mfx_qnet_destroy(self.handle)
+            self.handle = None
+
+    def pack(self, net):
+        return pack_qnet(net, self.F, self.A, self.use_mf, (self.blob_n, self.offsets))
+
+    def load(self, net):
+        """Upload the weights of torch QNet `net` (same shapes)."""
+        self._blob = self.pack(net).contiguous()
+        check(self._L.mfx_qnet_set_weights(self.handle, _ptr(self._blob), ctypes.c_size_t(self.blob_n), _stream()),
+              "mfx_qnet_set_weights")
+        return self
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, view, feature, prob=None, want_q=True):
+        """view [n, 13, 13, 7], feature [n, F], prob [n, A] (mean field) float32 CUDA tensors ->
+        (q [n, A] float32 or None, actions [n] int32 = argmax q)."""
+        n = view.shape[0]
+        view = view.reshape(n, -1).contiguous().float()
+        feature = feature.reshape(n, -1).contiguous().float()
+        if self.use_mf:
+            assert prob is not None and prob.shape[0] == n
+            prob = prob.reshape(n, -1).contiguous().float()
+        q = torch.empty((n, self.A), dtype=torch.float32, device=view.device) if want_q else None
+        act = torch.empty(n, dtype=torch.int32, device=view.device)
+        check(self._L.mfx_qnet_forward(self.handle, _ptr(view), _ptr(feature), _ptr(prob if self.use_mf else None),
+                                       int(n), _ptr(q), _ptr(act), _stream()), "mfx_qnet_forward")
+        return q, act
+
+    def act(self, view, feature, prob=None):
+        return self.forward(view, feature, prob, want_q=False)[1]
+
+    def act_rollout(self, eng, group):
+        """Actions of group `group` of a BattleBatch rollout from its current observation buffers and
+        former mean actions, written into the rollout's action buffer [E][G][rowcap] (live rows only)."""
+        E, rc, G = eng.n_envs, eng.rowcap, len(eng.handles)
+        if self._rows is None or self._rows.numel() < E * rc + 1:
+            self._rows = torch.empty(E * rc + 1, dtype=torch.int32, device="cuda")
+        ptr = {}
+        for name in ("view", "feature", "group_num", "mean_action", "actions"):
+            p, nb = _P(), ctypes.c_size_t()
+            eng._check(eng._dll.mfx_battle_rollout_buffer(eng.game, name.encode(), group if name in ("view", "feature")
+                                                          else 0, ctypes.byref(p), ctypes.byref(nb)), "rollout_buffer")
+            ptr[name] = p
+        stride = eng.mean_stride()
+        check(self._L.mfx_qnet_act_rollout(self.handle, ptr["view"], ptr["feature"], ptr["group_num"],
+                                           ptr["mean_action"], int(stride), int(E), int(G), int(group), int(rc),
+                                           _P(self._rows.data_ptr()), _P(self._rows.data_ptr() + 4 * E * rc),
+                                           ptr["actions"], _P(eng.stream_handle())), "mfx_qnet_act_rollout")
