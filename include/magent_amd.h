@@ -181,6 +181,13 @@ int mfx_qnet_act_rollout(void *handle, const float *d_view, const float *d_feat,
                          const double *d_mean, int mean_stride, int E, int G, int g, int rowcap, int32_t *d_rows,
                          int32_t *d_total, int32_t *d_act, void *stream);
 
+/* ---------------------------------------------------------------- part 6: replay rows */
+/* The data path of the replay buffers (algo/tools.py:26-362): for i < n, row idx[i] (or i; modulo src_mod
+ * when > 0) of every source column -> row dst_start + i (modulo dst_cap when > 0) of its destination column;
+ * n_cols <= 8, row_bytes per column; one launch (csrc/replay_kernels.hip). */
+int mfx_rows_copy(int n_cols, void *const *dst, const void *const *src, const int64_t *row_bytes, const int64_t *d_idx,
+                  int64_t src_mod, int64_t dst_start, int64_t dst_cap, int64_t n, void *stream);
+
 /* ---------------------------------------------------------------- library */
 const char *mfx_last_error(void);
 const char *mfx_build_info(void);

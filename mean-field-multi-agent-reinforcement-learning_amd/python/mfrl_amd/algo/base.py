@@ -9,7 +9,7 @@ import copy
 import numpy as np
 import torch
 
-from .. import mf
+from .. import mf, replay
 from .nets import QNet
 
 
@@ -126,14 +126,20 @@ class ValueNet:
     def _minibatch(self, buf, use_mean):
         """One sample + target + masked-MSE Adam step + soft update on the static index tensors."""
         i, j = self._s_idx, self._s_nxt
-        obs, feat = buf.obs0.data.index_select(0, i), buf.feat0.data.index_select(0, i)
-        obs_n, feat_n = buf.obs0.data.index_select(0, j), buf.feat0.data.index_select(0, j)
-        acts = buf.actions.data.index_select(0, i).long()
-        rew = buf.rewards.data.index_select(0, i)
-        done = buf.terminals.data.index_select(0, i)
-        mask = buf.masks.data.index_select(0, i).float()
-        prob = buf.prob.data.index_select(0, i) if use_mean else None
-        prob_n = buf.prob.data.index_select(0, j) if use_mean else None
+        # the minibatch rows: one HIP gather (k_rows_copy) per index list, into static tensors the
+        # captured graph reuses (allocated by the first, eager call)
+        cur = [buf.obs0, buf.feat0, buf.actions, buf.rewards, buf.terminals, buf.masks] + ([buf.prob] if use_mean else [])
+        nxt = [buf.obs0, buf.feat0] + ([buf.prob] if use_mean else [])
+        if getattr(self, "_mb", None) is None or self._mb[0][0].shape[0] != len(i):
+            self._mb = [[torch.empty((len(i),) + tuple(b.data.shape[1:]), dtype=b.data.dtype, device="cuda")
+                         for b in bufs] for bufs in (cur, nxt)]
+        replay.rows_copy(self._mb[0], [b.data for b in cur], i)
+        replay.rows_copy(self._mb[1], [b.data for b in nxt], j)
+        obs, feat, acts, rew, done, mask = self._mb[0][:6]
+        acts, mask = acts.long(), mask.float()
+        obs_n, feat_n = self._mb[1][:2]
+        prob = self._mb[0][6] if use_mean else None
+        prob_n = self._mb[1][2] if use_mean else None
         with torch.no_grad():
             t_q = self.target_net(obs_n, feat_n, prob_n)
             e_qn = self.eval_net(obs_n, feat_n, prob_n)
@@ -154,12 +160,21 @@ class ValueNet:
 
     @torch.no_grad()
     def act_dev(self, **kwargs):
-        """Device in, device out: int32 actions = argmax softmax(e_q / temperature)."""
+        """Device in, device out: int32 greedy actions (algo/base.py:228-254).  The Battle view runs the
+        hand-written HIP forward (mfrl_amd.policy.QNetHIP, csrc/policy_kernels.hip) with the eval net's
+        current weights: argmax of e_q, the reference's argmax softmax(e_q / temperature) up to float ties.
+        Other view shapes (not in the shipped configs) run the torch module."""
         view, feat = as_dev(kwargs["state"][0]), as_dev(kwargs["state"][1])
         self.temperature = kwargs["eps"]
         prob = self._prob(kwargs, len(view))
         if self.use_mf:
             assert len(prob) == len(view)
+        if self.view_space == (13, 13, 7) and self.num_actions <= 32:
+            if getattr(self, "_hip", None) is None:
+                from ..policy import QNetHIP
+                self._hip = QNetHIP(self.view_space, self.feature_space, self.num_actions, self.use_mf)
+            self._hip.load(self.eval_net)                # the weights train() last left
+            return self._hip.act(view, feat, prob)
         e_q = self.eval_net(view, feat, prob)
         return torch.argmax(torch.softmax(e_q / self.temperature, dim=1), dim=1).to(torch.int32)
 

@@ -13,12 +13,20 @@
 np.random is consumed exactly where the reference consumes it (agent shuffle, sample indices,
 push permutation), so a seeded run draws the same indices.  Keys are int64 agent ids (the batched
 engine passes env * cap + id).
+
+Every row move -- a push into the episode's step rows, tight()'s gather into the rings (with their wrap),
+sample()'s gather of a minibatch, EpisodesBuffer's per-agent gather -- is ONE launch of the HIP kernel
+k_rows_copy (mfrl_amd.replay.rows_copy, csrc/replay_kernels.hip) over all the columns it moves; torch
+computes only the index lists.  device='cpu' runs the same moves with torch indexing (the CPU tests of the
+semantics against the reference's fixtures; never a fallback for a missing library on the GPU).
 """
 import json
 import os
 
 import numpy as np
 import torch
+
+from .. import replay
 
 
 class Color:
@@ -31,6 +39,46 @@ def _dev(x, dtype, device="cuda"):
     if isinstance(x, torch.Tensor):
         return x.to(device=device, dtype=dtype)
     return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
+
+
+def _move(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
+    """rows_copy on the device (one HIP launch for every column); torch indexing for device='cpu'."""
+    if dst[0].is_cuda:
+        assert all(d.is_contiguous() for d in dst)
+        replay.rows_copy(dst, [x.contiguous() for x in src], idx, src_mod, dst_start, dst_cap, n)
+        return
+    if n is None:
+        n = len(idx) if idx is not None else len(src[0])
+    s = torch.arange(n) if idx is None else idx.to(torch.int64)
+    if src_mod:
+        s = s % src_mod
+    d = torch.arange(n) + dst_start
+    if dst_cap:
+        d = d % dst_cap
+    for a, b in zip(dst, src):
+        a[d] = b[s]
+
+
+def ring_append(bufs, srcs, idx=None):
+    """Append rows (srcs[k][idx], or srcs[k] in order) to MetaBuffers bufs[k], which share one position
+    (they are always appended together), in one move: only the last max_len rows survive, the ring wraps."""
+    n = len(idx) if idx is not None else len(srcs[0])
+    if n == 0:
+        return
+    b0 = bufs[0]
+    M = b0.max_len
+    start, skip = b0._flag, 0
+    if n > M:                                   # only the last max_len rows survive in the ring
+        skip = n - M
+        start = (start + skip) % M
+    if idx is not None:
+        idx = idx[skip:]
+    else:
+        srcs = [x[skip:] for x in srcs]
+    _move([b.data for b in bufs], srcs, idx, dst_start=start, dst_cap=M, n=n - skip)
+    for b in bufs:
+        b._flag = (start + n - skip) % M
+        b.length = min(b.length + n, M)
 
 
 class MetaBuffer:
@@ -46,28 +94,15 @@ class MetaBuffer:
         return self.length
 
     def sample(self, idx):
-        return self.data[idx % self.length]
+        out = torch.empty((len(idx),) + tuple(self.data.shape[1:]), dtype=self.data.dtype, device=self.device)
+        _move([out], [self.data], idx, src_mod=self.length)
+        return out
 
     def pull(self):
         return self.data[:self.length]
 
     def append(self, value):
-        value = _dev(value, self.data.dtype, self.device)
-        if len(value) > self.max_len:             # only the last max_len rows survive in the ring
-            skip = len(value) - self.max_len
-            self._flag = (self._flag + skip) % self.max_len
-            self.length = self.max_len
-            value = value[skip:]
-        num, start = len(value), 0
-        if self._flag + num > self.max_len:
-            tail = self.max_len - self._flag
-            self.data[self._flag:] = value[:tail]
-            num -= tail
-            start = tail
-            self._flag = 0
-        self.data[self._flag:self._flag + num] = value[start:]
-        self._flag += num
-        self.length = min(self.length + len(value), self.max_len)
+        ring_append([self], [_dev(value, self.data.dtype, self.device)])
 
 
 class _StepRows:
@@ -89,8 +124,9 @@ class _StepRows:
         if self.use_mean:
             spec["prob"] = ((self.act_n,), torch.float32)
         new = {k: torch.empty((cap,) + s, dtype=d, device=self.device) for k, (s, d) in spec.items()}
-        for k in self.cols:
-            new[k][:self.n] = self.cols[k][:self.n]
+        if self.n:
+            keys = list(self.cols)
+            _move([new[k] for k in keys], [self.cols[k] for k in keys], n=self.n)
         self.cols, self.cap = new, cap
 
     def push(self, ids, obs, feat, act, rew, alive, prob=None, order=None):
@@ -98,17 +134,15 @@ class _StepRows:
         ids = _dev(ids, torch.int64, dv)
         m = len(ids)
         sel = None if order is None else torch.as_tensor(order, device=dv, dtype=torch.int64)
-        pick = (lambda t: t) if sel is None else (lambda t: t.index_select(0, sel))
         self._ensure(self.n + m)
-        s = slice(self.n, self.n + m)
-        self.cols["ids"][s] = pick(ids)
-        self.cols["obs"][s] = pick(_dev(obs, torch.float32, dv).reshape((m,) + self.obs_shape))
-        self.cols["feat"][s] = pick(_dev(feat, torch.float32, dv).reshape((m,) + self.feat_shape))
-        self.cols["act"][s] = pick(_dev(act, torch.int32, dv).reshape(m))
-        self.cols["rew"][s] = pick(_dev(rew, torch.float32, dv).reshape(m))
-        self.cols["term"][s] = pick(~_dev(alive, torch.bool, dv).reshape(m))
+        keys = ["ids", "obs", "feat", "act", "rew", "term"]
+        src = [ids, _dev(obs, torch.float32, dv).reshape((m,) + self.obs_shape),
+               _dev(feat, torch.float32, dv).reshape((m,) + self.feat_shape), _dev(act, torch.int32, dv).reshape(m),
+               _dev(rew, torch.float32, dv).reshape(m), ~_dev(alive, torch.bool, dv).reshape(m)]
         if self.use_mean:
-            self.cols["prob"][s] = pick(_dev(prob, torch.float32, dv).reshape(m, self.act_n))
+            keys.append("prob")
+            src.append(_dev(prob, torch.float32, dv).reshape(m, self.act_n))
+        _move([self.cols[k] for k in keys], src, sel, dst_start=self.n, n=m)
         self.n += m
 
     def grouped(self, key_order=None):
@@ -185,17 +219,16 @@ class MemoryGroup:
             order = order[keep][torch.argsort(key)]
             counts = torch.clamp(counts, max=self.sub_len)
         c = rows.cols
-        term = c["term"].index_select(0, order)
-        mask = ~term
-        mask[torch.cumsum(counts, 0) - 1] = False     # last row of every agent's sequence
-        self.obs0.append(c["obs"].index_select(0, order))
-        self.feat0.append(c["feat"].index_select(0, order))
-        self.actions.append(c["act"].index_select(0, order))
-        self.rewards.append(c["rew"].index_select(0, order))
-        self.terminals.append(term)
+        # masks = not terminal and not the last row of an agent's sequence, laid out in step-row order so
+        # that every column moves with the same gather
+        mask = ~c["term"][:rows.n]
+        mask[order[torch.cumsum(counts, 0) - 1]] = False
+        bufs = [self.obs0, self.feat0, self.actions, self.rewards, self.terminals, self.masks]
+        srcs = [c["obs"], c["feat"], c["act"], c["rew"], c["term"], mask]
         if self.use_mean:
-            self.prob.append(c["prob"].index_select(0, order))
-        self.masks.append(mask)
+            bufs.append(self.prob)
+            srcs.append(c["prob"])
+        ring_append(bufs, srcs, order)
         self._new_add += len(order)
         rows.clear()
 
@@ -208,13 +241,23 @@ class MemoryGroup:
         next_idx = (idx + 1) % self.nb_entries
         idx = torch.as_tensor(idx, device=self.device)
         next_idx = torch.as_tensor(next_idx, device=self.device)
-        obs, obs_next = self.obs0.sample(idx), self.obs0.sample(next_idx)
-        feature, feature_next = self.feat0.sample(idx), self.feat0.sample(next_idx)
-        actions, rewards = self.actions.sample(idx), self.rewards.sample(idx)
-        dones, masks = self.terminals.sample(idx), self.masks.sample(idx)
+        B = len(idx)
+        cur = [self.obs0, self.feat0, self.actions, self.rewards, self.terminals, self.masks]
+        nxt = [self.obs0, self.feat0]
         if self.use_mean:
-            return (obs, feature, actions, self.prob.sample(idx), obs_next, feature_next, self.prob.sample(next_idx),
-                    rewards, dones, masks)
+            cur.append(self.prob)
+            nxt.append(self.prob)
+
+        def gather(bufs, ix):                   # one move for every column sampled at these indices
+            out = [torch.empty((B,) + tuple(b.data.shape[1:]), dtype=b.data.dtype, device=self.device) for b in bufs]
+            _move(out, [b.data for b in bufs], ix, src_mod=self.nb_entries)
+            return out
+
+        c, x = gather(cur, idx), gather(nxt, next_idx)
+        obs, feature, actions, rewards, dones, masks = c[:6]
+        obs_next, feature_next = x[:2]
+        if self.use_mean:
+            return obs, feature, actions, c[6], obs_next, feature_next, x[2], rewards, dones, masks
         return obs, feature, obs_next, feature_next, dones, rewards, actions, masks
 
     def get_batch_num(self):
@@ -251,8 +294,11 @@ class EpisodesBuffer:
         if self._rows is None or self._rows.n == 0:
             return None
         order, counts, keys = self._rows.grouped()
-        out = {k: v.index_select(0, order) for k, v in self._rows.cols.items() if k in self._rows.cols}
-        return out, counts
+        names = list(self._rows.cols)
+        out = [torch.empty((len(order),) + tuple(self._rows.cols[k].shape[1:]), dtype=self._rows.cols[k].dtype,
+                           device=self.device) for k in names]
+        _move(out, [self._rows.cols[k] for k in names], order)
+        return dict(zip(names, out)), counts
 
 
 class SummaryObj:

@@ -1,0 +1,39 @@
+"""Row moves of the device replay buffers (mfrl_amd.algo.tools) on the HIP kernel k_rows_copy
+(csrc/replay_kernels.hip): every push / tight / sample of MemoryGroup and EpisodesBuffer (algo/tools.py:26-362)
+is one launch that gathers whole rows of all its columns.  CUDA tensors only; a missing engine library raises.
+"""
+import ctypes
+
+import torch
+
+from . import check, lib
+
+_MAX_COLS = 8
+
+
+def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
+    """For i < n: row (idx[i] if idx is not None else i), taken modulo src_mod if > 0, of every tensor in
+    `src` -> row dst_start + i (modulo dst_cap if > 0) of the matching tensor in `dst`.  Tensors: CUDA,
+    contiguous, first dimension = rows, equal row byte sizes pairwise."""
+    assert len(dst) == len(src) and 0 < len(dst) <= _MAX_COLS
+    if n is None:
+        n = len(idx) if idx is not None else src[0].shape[0]
+    if n == 0:
+        return
+    rb = []
+    for d, s in zip(dst, src):
+        assert d.is_cuda and s.is_cuda and d.is_contiguous() and s.is_contiguous(), "rows_copy: contiguous CUDA tensors"
+        b = d.element_size() * (d[0].numel() if d.dim() > 1 else 1)
+        assert b == s.element_size() * (s[0].numel() if s.dim() > 1 else 1), "rows_copy: row sizes differ"
+        rb.append(b)
+    if idx is not None:
+        idx = idx.to(device=dst[0].device, dtype=torch.int64).contiguous()
+    k = len(dst)
+    L = lib()
+    L.mfx_rows_copy.restype = ctypes.c_int
+    P = ctypes.c_void_p * k
+    check(L.mfx_rows_copy(k, P(*[d.data_ptr() for d in dst]), P(*[s.data_ptr() for s in src]),
+                          (ctypes.c_int64 * k)(*rb), ctypes.c_void_p(idx.data_ptr() if idx is not None else 0),
+                          ctypes.c_int64(int(src_mod)), ctypes.c_int64(int(dst_start)), ctypes.c_int64(int(dst_cap)),
+                          ctypes.c_int64(int(n)), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+          "mfx_rows_copy")

@@ -1,0 +1,45 @@
+"""The replay rows' HIP mover (mfx_rows_copy, csrc/replay_kernels.hip) against torch indexing: gathers with and
+without an index list, modulo a source length, into a ring with wrap; column widths that take the 16-B,
+4-B and byte paths (view rows of 4,732 B, int32, bool, float64 x 21).  The buffers' semantics against the
+reference's own MemoryGroup / EpisodesBuffer: test_algo_gpu.py::test_device_replay_matches_reference_fixture."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cols(n, gen):
+    return [torch.rand((n, 13, 13, 7), generator=gen, device="cuda"),            # 4,732 B: 4-B path
+            torch.randint(0, 21, (n,), generator=gen, device="cuda", dtype=torch.int32),
+            torch.rand((n,), generator=gen, device="cuda") < 0.5,                 # 1 B: byte path
+            torch.rand((n, 4), generator=gen, device="cuda"),                     # 16 B: 16-B path
+            torch.rand((n, 21), generator=gen, device="cuda", dtype=torch.float64)]
+
+
+@pytest.mark.parametrize("n_src,n,cap,start,mod", [(1000, 1000, 0, 0, 0), (1000, 700, 2000, 1500, 0),
+                                                   (300, 257, 300, 250, 300), (50, 1, 0, 7, 0)])
+def test_rows_copy_matches_torch_indexing(n_src, n, cap, start, mod):
+    from mfrl_amd.replay import rows_copy
+    gen = torch.Generator(device="cuda").manual_seed(n + start)
+    src = _cols(n_src, gen)
+    n_dst = cap if cap else start + n
+    dst = [torch.zeros((n_dst,) + tuple(x.shape[1:]), dtype=x.dtype, device="cuda") for x in src]
+    want = [d.clone() for d in dst]
+    idx = torch.randint(-3 * n_src, 3 * n_src, (n,), generator=gen, device="cuda") if mod else \
+        torch.randperm(n_src, generator=gen, device="cuda")[:n]
+    rows_copy(dst, src, idx, src_mod=mod, dst_start=start, dst_cap=cap)
+    s = (idx % mod) if mod else idx
+    d = torch.arange(n, device="cuda") + start
+    if cap:
+        d = d % cap
+    for w, x in zip(want, src):
+        w[d] = x[s]
+    torch.cuda.synchronize()
+    for a, b in zip(dst, want):
+        assert torch.equal(a, b)
+    # no index list: rows 0..n-1 in order
+    dst2 = [torch.zeros_like(x[:n]) for x in src]
+    rows_copy(dst2, [x[:n].contiguous() for x in src])
+    torch.cuda.synchronize()
+    for a, x in zip(dst2, src):
+        assert torch.equal(a, x[:n])
