@@ -15,9 +15,9 @@
 //   k_qnet_conv  one wave per agent: the view staged in LDS, Conv1 as an implicit GEMM over 121
 //                positions x 32 channels x K 63 (padded to 64), its output kept in LDS, Conv2 as an
 //                implicit GEMM over 81 positions x 32 x K 288; the 2,592 activations to HBM (10 KB/agent)
-//   k_qnet_head  four waves x 16 agents per workgroup: Dense-Obs as a GEMM (K 2,592) with the weight
-//                chunks staged once per workgroup in LDS and shared by the four waves, then the small
-//                layers the same way, the Q values and the argmax
+//   k_qnet_head  four waves x 16 agents per workgroup: every layer transposed (weights as the A operand),
+//                so each layer's accumulators are the next layer's B operand in registers; the weight
+//                chunks staged in LDS and shared by the four waves; the Q values and the argmax
 // A and B operands of v_mfma_f32_16x16x4_f32: lane l holds A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15];
 // D: lane l holds D[(l >> 4) * 4 + r][l & 15], r = 0..3 (cdna_hip_programming.md, fragment layout).
 #include <hip/hip_runtime.h>
@@ -39,8 +39,6 @@ constexpr int kQK1 = 64;                                 // conv1 K: 3 * 3 * 7 =
 constexpr int kQK2 = 3 * 3 * kQCh;                       // conv2 K: 288
 constexpr int kQFlat = kQC2 * kQC2 * kQCh;               // 2,592
 constexpr int kQHObs = 256, kQHEmb = 32, kQHP1 = 64, kQHP2 = 32, kQH2 = 128, kQHOut = 64, kQMaxA = 32;
-constexpr int kQActW = kQHObs + kQHEmb + kQHP2;          // concat width, mean field (288 without)
-constexpr int kQActLd = kQActW + 4;                      // LDS row stride of the activations (bank spread)
 
 // Device view of one packed weight blob (layout: QNetLayout; every matrix [K][N] row-major, K padded to a
 // multiple of 4 with zero rows, N of the Q layer padded to 32 with zero columns).
@@ -59,10 +57,13 @@ __device__ __forceinline__ void qwave_sync() {
 }
 
 // ------------------------------------------------------------------------------------------ conv
-// LDS: w1 [64][32], w2 [288][32] (shared), per wave the view [1,184] and conv1's output [121][32].
+// LDS: w1 [64][32], w2 [288][48] (shared), per wave the view [1,184] and conv1's output [121][34].  Row
+// strides chosen for the banks (ds_read_b32: 32 banks per half-wave of 16 rows x 2 k): w2's 48 (16 mod
+// 32) puts the two k rows of a half-wave on different banks, conv1's 34 (2 mod 32) the 16 positions.
 constexpr int kQConvWaves = 4;
-constexpr int kQViewLds = 1184, kQC1Lds = kQC1 * kQC1 * kQCh;
-constexpr size_t kQConvSmem = (size_t)(kQK1 * kQCh + kQK2 * kQCh + kQConvWaves * (kQViewLds + kQC1Lds)) * 4;
+constexpr int kQW2Ld = 48, kQC1Ld = 34;
+constexpr int kQViewLds = 1184, kQC1Lds = kQC1 * kQC1 * kQC1Ld;
+constexpr size_t kQConvSmem = (size_t)(kQK1 * kQCh + kQK2 * kQW2Ld + kQConvWaves * (kQViewLds + kQC1Lds)) * 4;
 
 // Offset of im2col column k (ky, kx, ci) in the staged 13 x 13 x 7 view; the pad column 63 reads
 // element 0 against a zero weight row.
@@ -79,10 +80,10 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
     float* w1 = qsm;
     float* w2 = w1 + kQK1 * kQCh;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
-    float* vs = w2 + kQK2 * kQCh + wid * (kQViewLds + kQC1Lds);
+    float* vs = w2 + kQK2 * kQW2Ld + wid * (kQViewLds + kQC1Lds);
     float* c1 = vs + kQViewLds;
     for (int i = threadIdx.x; i < kQK1 * kQCh; i += blockDim.x) w1[i] = p.w1[i];
-    for (int i = threadIdx.x; i < kQK2 * kQCh; i += blockDim.x) w2[i] = p.w2[i];
+    for (int i = threadIdx.x; i < kQK2 * kQCh; i += blockDim.x) w2[(i / kQCh) * kQW2Ld + i % kQCh] = p.w2[i];
     __syncthreads();
     // conv1's B operands for all 16 k-steps stay in registers, so do the lane's im2col offsets
     float b1r[16][2];
@@ -94,10 +95,28 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
         koff[kk] = conv1_koff(kk * 4 + h);
     }
     const float bias1a = p.b1[c], bias1b = p.b1[16 + c], bias2a = p.b2[c], bias2b = p.b2[16 + c];
-    for (int i = blockIdx.x * kQConvWaves + wid; i < n; i += gridDim.x * kQConvWaves) {
+    // the next agent's view is in flight in registers while this one is computed (19 floats per lane)
+    constexpr int kVR = (kQViewF + 63) / 64;
+    float vr[kVR];
+    auto fetch = [&](int i) {
+        if (i >= n) return;
         const float* src = view + (size_t)(rows ? rows[i] : i) * view_ld;
-        for (int q = lane; q < kQViewF; q += 64) vs[q] = src[q];
+#pragma unroll
+        for (int j = 0; j < kVR; ++j) {
+            const int q = lane + j * 64;
+            vr[j] = q < kQViewF ? src[q] : 0.f;
+        }
+    };
+    const int step = gridDim.x * kQConvWaves;
+    fetch(blockIdx.x * kQConvWaves + wid);
+    for (int i = blockIdx.x * kQConvWaves + wid; i < n; i += step) {
+#pragma unroll
+        for (int j = 0; j < kVR; ++j) {
+            const int q = lane + j * 64;
+            if (q < kQViewF) vs[q] = vr[j];
+        }
         qwave_sync();
+        fetch(i + step);
         // ---- Conv1: 8 position tiles (121 of 128 rows) x 2 channel tiles, K 64
         for (int mt = 0; mt < 8; ++mt) {
             const int pa = min(mt * 16 + c, kQC1 * kQC1 - 1);
@@ -113,8 +132,8 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
             for (int r = 0; r < 4; ++r) {
                 const int pos = mt * 16 + h * 4 + r;
                 if (pos < kQC1 * kQC1) {
-                    c1[pos * kQCh + c] = fmaxf(d0[r] + bias1a, 0.f);
-                    c1[pos * kQCh + 16 + c] = fmaxf(d1[r] + bias1b, 0.f);
+                    c1[pos * kQC1Ld + c] = fmaxf(d0[r] + bias1a, 0.f);
+                    c1[pos * kQC1Ld + 16 + c] = fmaxf(d1[r] + bias1b, 0.f);
                 }
             }
         }
@@ -126,13 +145,15 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
 #pragma unroll
         for (int mt = 0; mt < 6; ++mt) {
             const int pa = min(mt * 16 + c, kQC2 * kQC2 - 1);
-            cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQCh + h;
+            cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQC1Ld + h;
             acc[mt][0] = {0.f, 0.f, 0.f, 0.f};
             acc[mt][1] = {0.f, 0.f, 0.f, 0.f};
         }
-        for (int kk = 0; kk < kQK2 / 4; ++kk) {
-            const int so = ((kk / 24) * kQC1 + (kk / 8) % 3) * kQCh + (kk % 8) * 4;
-            const float b0 = w2[(kk * 4 + h) * kQCh + c], b1 = w2[(kk * 4 + h) * kQCh + 16 + c];
+#pragma unroll 4
+        for (int kk = 0; kk < kQK2 / 4; ++kk) {              // (unrolled: the next k-steps' LDS reads issue
+                                                             //  under this one's MFMAs)
+            const int so = ((kk / 24) * kQC1 + (kk / 8) % 3) * kQC1Ld + (kk % 8) * 4;
+            const float b0 = w2[(kk * 4 + h) * kQW2Ld + c], b1 = w2[(kk * 4 + h) * kQW2Ld + 16 + c];
 #pragma unroll
             for (int mt = 0; mt < 6; ++mt) {
                 const float a = c1[cb[mt] + so];
@@ -156,54 +177,75 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
 }
 
 // ------------------------------------------------------------------------------------------ head
-// One workgroup = 4 waves x 16 agents.  wg_gemm: every wave multiplies ITS 16 rows of A (a functor of
-// the k-step) by the same B [K][NT * 16], whose 16-row chunks the whole workgroup stages in LDS (double
-// buffered), accumulating into acc[NT].  Call sites are uniform across the workgroup (barriers inside).
-constexpr int kQHeadWaves = 4, kQKC = 16;                // agents per wave = 16; B rows per chunk
-constexpr int kQBLd = kQHObs + 16;                       // LDS stride of a B chunk row (bank spread)
-constexpr size_t kQHeadSmem = (size_t)(2 * kQKC * kQBLd + kQHeadWaves * 16 * kQActLd + kQHeadWaves * 16 * kQHP1) * 4;
+// One workgroup = 4 waves x 16 agents.  Every layer is computed TRANSPOSED, out^T [N_out x 16 agents] =
+// W^T [N_out x K] . in^T [K x 16]: the weights are the A operand (rows = output units on the lane's column
+// index), the layer input the B operand (agents on the lane's column index).  The accumulator tile then has
+// the agents on its lanes and the output units in its registers, which is exactly the B operand the next
+// layer needs -- "an accumulator tile as the next MFMA's operand" (cdna_hip_programming.md): the
+// activations never leave the registers, with the k order inside each 16-row chunk permuted to match
+// (k-step s of chunk t takes units 16 t + 4 h + s, lane group h supplying its register s).  The weights
+// are staged per 16-row chunk in LDS (double buffered, the next chunk in flight in registers) and shared
+// by the four waves; LDS holds nothing else.
+constexpr int kQHeadWaves = 4, kQKC = 16;                // agents per wave = 16; weight rows per chunk
+constexpr int kQBLd = kQHObs + 16;                       // LDS stride of a staged row (16 mod 32: the 4 rows
+                                                         //   of a k-step fall on distinct banks per half-wave)
+constexpr size_t kQHeadSmem = (size_t)2 * kQKC * kQBLd * 4;
 
-template <int NT, class AF>
-__device__ __forceinline__ void wg_gemm(const float* __restrict__ B, int K, AF a_at, float* bsm, f32x4* acc) {
-    constexpr int N = NT * 16;
+// acc[MT] = W^T . V over K (K a multiple of 4, rows of W past K read as zero).  W: [K][MT * 16] row-major.
+// v_at(ch, s): this lane's B operand for k = 16 ch + 4 h + s (agent = lane & 15).  NCH > 0: the chunk loop
+// is unrolled (K <= 16 NCH), so a v_at that indexes the previous layer's accumulators by ch stays in
+// registers.  Uniform call sites (barriers inside).
+template <int MT, int NCH = 0, class VF>
+__device__ __forceinline__ void wg_gemm_t(const float* __restrict__ W, int K, VF v_at, float* bsm, f32x4* acc) {
+    constexpr int N = MT * 16;                           // staged row width; 16 rows = MT floats per thread
     const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
     const int nchunk = (K + kQKC - 1) / kQKC;
-    auto stage = [&](int ch, float* dst) {               // rows [ch * 16, +16) of B (zero past K)
-        for (int q = threadIdx.x; q < kQKC * N; q += blockDim.x) {
-            const int r = q / N, col = q - r * N, k = ch * kQKC + r;
-            dst[r * kQBLd + col] = k < K ? B[(size_t)k * N + col] : 0.f;
+    float pre[MT];
+    auto load = [&](int ch) {
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int q = threadIdx.x + j * 256, r = q / N, col = q - r * N, k = ch * kQKC + r;
+            pre[j] = k < K ? W[(size_t)k * N + col] : 0.f;
+        }
+    };
+    auto store = [&](float* dst) {
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int q = threadIdx.x + j * 256, r = q / N, col = q - r * N;
+            dst[r * kQBLd + col] = pre[j];
         }
     };
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-    stage(0, bsm);
+    for (int t = 0; t < MT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+    load(0);
+    store(bsm);
     __syncthreads();
-    for (int ch = 0; ch < nchunk; ++ch) {
-        float* cur = bsm + (ch & 1) * kQKC * kQBLd;
-        if (ch + 1 < nchunk) stage(ch + 1, bsm + ((ch + 1) & 1) * kQKC * kQBLd);
+    auto chunk = [&](int ch) {
+        const float* cur = bsm + (ch & 1) * kQKC * kQBLd;
+        if (ch + 1 < nchunk) load(ch + 1);               // in flight during this chunk's MFMAs
 #pragma unroll
-        for (int s = 0; s < kQKC / 4; ++s) {
-            const int kk = ch * (kQKC / 4) + s;
-            if (kk * 4 >= K) break;
-            const float a = a_at(kk);
-            const float* brow = cur + (s * 4 + h) * kQBLd + c;
+        for (int s = 0; s < 4; ++s) {
+            const float v = v_at(ch, s);
+            const float* arow = cur + (4 * h + s) * kQBLd + c;
 #pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = mfma4(a, brow[t * 16], acc[t]);
+            for (int t = 0; t < MT; ++t) acc[t] = mfma4(arow[t * 16], v, acc[t]);
         }
+        if (ch + 1 < nchunk) store(bsm + ((ch + 1) & 1) * kQKC * kQBLd);
         __syncthreads();
+    };
+    if constexpr (NCH > 0) {
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch)
+            if (ch < nchunk) chunk(ch);
+    } else {
+        for (int ch = 0; ch < nchunk; ++ch) chunk(ch);
     }
 }
 
-// Write relu(acc + bias) of NT tiles into this wave's activation rows at column col0.
-template <int NT>
-__device__ __forceinline__ void put_relu(const f32x4* acc, const float* __restrict__ bias, float* act, int ld, int col0) {
-    const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const float b = bias[t * 16 + c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) act[(h * 4 + r) * ld + col0 + t * 16 + c] = fmaxf(acc[t][r] + b, 0.f);
-    }
+// relu(acc + bias) of unit 16 t + 4 h + s: the B operand of the next layer's chunk t, k-step s.
+__device__ __forceinline__ float relu_unit(const f32x4* acc, const float* __restrict__ bias, int t, int s) {
+    const int h = (threadIdx.x & 63) >> 4;
+    return fmaxf(acc[t][s] + bias[16 * t + 4 * h + s], 0.f);
 }
 
 // Compact agent i -> (view row, action slot, prob row): rows == null: (i, i, i); else row = rows[i]
@@ -214,76 +256,89 @@ struct QRowMap {
 };
 
 template <typename PT>
-__global__ void __launch_bounds__(256, 1) k_qnet_head(QNetDev p, const float* __restrict__ conv, int n,
+__global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __restrict__ conv, int n,
                                                       const float* __restrict__ feat, size_t feat_ld,
                                                       const PT* __restrict__ prob, size_t prob_ld, QRowMap rm,
                                                       float* __restrict__ q_out, int32_t* __restrict__ act_out) {
     extern __shared__ __attribute__((aligned(16))) float qsm[];
     float* bsm = qsm;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
-    float* act = bsm + 2 * kQKC * kQBLd + wid * 16 * kQActLd;            // [16][kQActLd]
-    float* tmp = bsm + 2 * kQKC * kQBLd + kQHeadWaves * 16 * kQActLd + wid * 16 * kQHP1;   // [16][64]
     const int base = (blockIdx.x * kQHeadWaves + wid) * 16;
-    const int ia = min(base + c, n - 1);                 // this lane's A row (clamped: junk rows, never written)
+    const int ia = min(base + c, n - 1);                 // this lane's agent (clamped: junk rows, never written)
     const int row = rm.rows ? rm.rows[ia] : ia;
     const int env = rm.rows ? row / rm.rowcap : ia;
-    f32x4 acc[16];
-    // ---- Dense-Obs: [16 x 2592] x [2592 x 256]
+    // ---- Dense-Obs^T [256 x 16]: the conv activations of this lane's agent, 4 consecutive per chunk step
+    f32x4 hobs[16];
     {
-        const float* ar = conv + (size_t)ia * kQFlat + h;
-        wg_gemm<16>(p.wd, kQFlat, [&](int kk) { return ar[kk * 4]; }, bsm, acc);
-        put_relu<16>(acc, p.bd, act, kQActLd, 0);
+        const float4* ar = reinterpret_cast<const float4*>(conv + (size_t)ia * kQFlat) + h;   // k = 16 ch + 4 h + s
+        float4 cur4 = ar[0], nxt4 = cur4;
+        int have = 0;
+        wg_gemm_t<16>(p.wd, kQFlat, [&](int ch, int s) {
+            if (s == 0) {                                // chunk ch's four values; chunk ch + 1's in flight
+                if (have != ch) cur4 = nxt4;
+                have = ch;
+                if ((ch + 1) * kQKC < kQFlat) nxt4 = ar[(ch + 1) * 4];
+            }
+            return s == 0 ? cur4.x : s == 1 ? cur4.y : s == 2 ? cur4.z : cur4.w;
+        }, bsm, hobs);
     }
-    // ---- Dense-Emb: [16 x F] x [F x 32]
+    // ---- Dense-Emb^T [32 x 16]
+    f32x4 hemb[2];
     {
         const float* fr = feat + (size_t)row * feat_ld;
         const int F = p.F;
-        wg_gemm<2>(p.we, p.Fp, [&](int kk) { const int k = kk * 4 + h; return k < F ? fr[k] : 0.f; }, bsm, acc);
-        put_relu<2>(acc, p.be, act, kQActLd, kQHObs);
+        wg_gemm_t<2>(p.we, p.Fp, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < F ? fr[k] : 0.f; },
+                     bsm, hemb);
     }
-    // ---- mean field: Prob-Emb 64, Dense-Act-Prob 32 (the prob input cast to float32 as the placeholder does)
+    // ---- mean field: Prob-Emb^T [64 x 16], Dense-Act-Prob^T [32 x 16] (prob cast to float32 as the placeholder does)
+    f32x4 hp[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     if (p.use_mf) {
         const PT* pr = prob + (size_t)env * prob_ld;
         const int A = p.A;
-        wg_gemm<4>(p.wp1, p.Ap, [&](int kk) { const int k = kk * 4 + h; return k < A ? (float)pr[k] : 0.f; }, bsm, acc);
-        put_relu<4>(acc, p.bp1, tmp, kQHP1, 0);
-        qwave_sync();
-        wg_gemm<2>(p.wp2, kQHP1, [&](int kk) { return tmp[c * kQHP1 + kk * 4 + h]; }, bsm, acc);
-        put_relu<2>(acc, p.bp2, act, kQActLd, kQHObs + kQHEmb);
+        f32x4 p1[4];
+        wg_gemm_t<4>(p.wp1, p.Ap, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < A ? (float)pr[k] : 0.f; },
+                     bsm, p1);
+        wg_gemm_t<2, kQHP1 / 16>(p.wp2, kQHP1, [&](int ch, int s) { return relu_unit(p1, p.bp1, ch, s); }, bsm, hp);
     }
-    qwave_sync();
-    // ---- Dense2 128, Dense-Out 64 (tmp), Q-Value
-    wg_gemm<8>(p.w2d, p.Kc, [&](int kk) { return act[c * kQActLd + kk * 4 + h]; }, bsm, acc);
-    qwave_sync();
-    put_relu<8>(acc, p.b2d, act, kQActLd, 0);           // (the concat row is consumed: reuse it)
-    qwave_sync();
-    wg_gemm<4>(p.wo, kQH2, [&](int kk) { return act[c * kQActLd + kk * 4 + h]; }, bsm, acc);
-    put_relu<4>(acc, p.bo, tmp, kQHP1, 0);
-    qwave_sync();
-    wg_gemm<2>(p.wq, kQHOut, [&](int kk) { return tmp[c * kQHP1 + kk * 4 + h]; }, bsm, acc);
-    // Q values to LDS (reusing act), then one lane per agent: output and argmax (first maximum)
+    // ---- Dense2^T [128 x 16] over concat(h_obs 256, h_emb 32, h_prob 32): chunk ch < 16 is h_obs tile ch,
+    // 16-17 h_emb, 18-19 h_prob
+    f32x4 d2[8];
+    wg_gemm_t<8, (kQHObs + kQHEmb + kQHP2) / 16>(p.w2d, p.Kc, [&](int ch, int s) {
+        if (ch < 16) return relu_unit(hobs, p.bd, ch, s);
+        if (ch < 18) return relu_unit(hemb, p.be, ch - 16, s);
+        return relu_unit(hp, p.bp2, ch - 18, s);
+    }, bsm, d2);
+    f32x4 d3[4];
+    wg_gemm_t<4, kQH2 / 16>(p.wo, kQH2, [&](int ch, int s) { return relu_unit(d2, p.b2d, ch, s); }, bsm, d3);
+    f32x4 qv[2];
+    wg_gemm_t<2, kQHOut / 16>(p.wq, kQHOut, [&](int ch, int s) { return relu_unit(d3, p.bo, ch, s); }, bsm, qv);
+    // ---- Q values: lane (h, c) holds actions 16 t + 4 h + r of agent c; argmax (first maximum) over the
+    // four lanes of the agent
+    const int A = p.A;
+    float best = -__builtin_huge_valf();
+    int bi = 1 << 30;
+    const int i = base + c;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const float b = p.bq[t * 16 + c];
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) act[(h * 4 + r) * kQActLd + t * 16 + c] = acc[t][r] + b;
+        for (int r = 0; r < 4; ++r) {
+            const int a = 16 * t + 4 * h + r;
+            if (a < A) {
+                const float x = qv[t][r] + p.bq[a];
+                if (q_out && i < n) q_out[(size_t)i * A + a] = x;
+                if (x > best || (x == best && a < bi)) { best = x; bi = a; }
+            }
+        }
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {                  // lanes c, c + 16, c + 32, c + 48
+        const float ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
-    qwave_sync();
-    if (lane < 16 && base + lane < n) {
-        const int i = base + lane;
-        const float* qr = act + lane * kQActLd;
-        int best = 0;
-        float bv = qr[0];
-        for (int k = 0; k < p.A; ++k) {
-            const float x = qr[k];
-            if (q_out) q_out[(size_t)i * p.A + k] = x;
-            if (x > bv) { bv = x; best = k; }
-        }
-        if (act_out) {
-            const int r = rm.rows ? rm.rows[i] : i;
-            const size_t slot = rm.rows ? (size_t)(r / rm.rowcap) * rm.act_env + rm.act_off + r % rm.rowcap : (size_t)i;
-            act_out[slot] = best;
-        }
+    if (h == 0 && i < n && act_out) {
+        const int r = rm.rows ? rm.rows[i] : i;
+        const size_t slot = rm.rows ? (size_t)(r / rm.rowcap) * rm.act_env + rm.act_off + r % rm.rowcap : (size_t)i;
+        act_out[slot] = bi;
     }
 }
 
