@@ -398,6 +398,7 @@ def main():
     eng = BattleBatch(args.map, E, stream=stream)
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
+    grid, lds = eng.rollout_info()          # persistent grid, LDS bytes per workgroup
     S = max(1, args.substeps if args.substeps is not None else (16 if path == "k_rollout_bigq" else 4))
     if S != 1:
         eng.rollout_substeps(S)
@@ -490,7 +491,8 @@ def main():
                          "kernel": kern, "kernel_ms": kernel_ms,
                          "kernel_ms_is": "mean launch duration (HIP events on the launch stream), %d step(s) per launch"
                                          % S,
-                         "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch},
+                         "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch,
+                         "grid": grid, "lds_bytes": lds},
             "cpu_baseline": None,
             "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],
                          "kills": red[3], "note": "all ranks, since rollout_init (RCCL all-reduce per episode batch)"},
