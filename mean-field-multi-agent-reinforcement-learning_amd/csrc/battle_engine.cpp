@@ -432,7 +432,6 @@ public:
         }
         if (t.width < 1 || t.length < 1 || t.width > 8 || t.length > 8)
             return fail("agent bodies must be 1..8 cells wide and long");
-        if (t.can_absorb) return fail("can_absorb is not supported");
         const int parity = t.width % 2;
         if (t.view_angle >= 180) {
             if (std::fabs(t.view_angle - 360) > 1e-5) return fail("only angle = 360 when angle > 180");
@@ -646,6 +645,7 @@ public:
             T.hp = t.hp; T.damage = t.damage; T.step_recover = t.step_recover; T.kill_supply = t.kill_supply;
             T.step_reward = t.step_reward; T.kill_reward = t.kill_reward; T.dead_penalty = t.dead_penalty;
             T.attack_penalty = t.attack_penalty; T.attack_in_group = t.attack_in_group;
+            T.can_absorb = t.can_absorb;
             T.n_action = t.n_action; T.turn_base = t.turn_base; T.attack_base = t.attack_base;
             T.n_move = t.move.count; T.n_attack = t.attack.count;
             T.view_w = t.view.w; T.view_h = t.view.h;
@@ -694,7 +694,8 @@ public:
         p.record_events = first_render ? 0 : 1;
         p.par_step = 1;
         for (int g = 0; g < p.n_groups; g++)
-            p.par_step &= p.type[g].kill_supply == 0.0f && p.type[g].body_w == 1 && p.type[g].body_h == 1;
+            p.par_step &= p.type[g].kill_supply == 0.0f && p.type[g].body_w == 1 && p.type[g].body_h == 1 &&
+                          !p.type[g].can_absorb;            // absorption: the serial move (do_move_one)
         if (turn || food) p.par_step = 0;
         gp = p;
         return 0;
@@ -1078,6 +1079,8 @@ public:
         if (turn || food) return fail("rollout: turn_mode / food_mode need the per-call API");
         for (int g = 0; g < G; g++)
             if (gp.type[g].body_w != 1 || gp.type[g].body_h != 1) return fail("rollout: 1x1 bodies only; use the per-call API");
+        for (int g = 0; g < G; g++)
+            if (gp.type[g].can_absorb) return fail("rollout: can_absorb types need the per-call API");
         try {
             ensure_capacity(total, total);
             {
@@ -1990,8 +1993,17 @@ public:
                 for (int i = 1; i <= walls[0]; i++) fout << walls[2 * i] << " " << walls[2 * i + 1] << std::endl;
             }
             std::vector<int> ev = attack_events();
+            // can_absorb groups: only their absorbed agents are drawn (RenderGenerator.cc:129-160)
+            std::vector<std::vector<int>> absorbed((size_t)G);
             int num_agents = 0;
-            for (int i = 0; i < G; i++) num_agents += allocated ? num_env0(i) : 0;
+            for (int i = 0; i < G && allocated; i++) {
+                const int n = num_env0(i);
+                num_agents += n;
+                if (!gtype(i).can_absorb || !n) continue;
+                absorbed[i].resize(n);
+                MFX_CHECK(host_get(i, kGetAbsorbed, absorbed[i].data(), 4));
+                for (int j = 0; j < n; j++) num_agents -= absorbed[i][j] ? 0 : 1;
+            }
             fout << "F" << " " << num_agents << " " << (int)(ev.size() / 3) << " " << 0 << std::endl;
             for (int i = 0; i < G && allocated; i++) {
                 const int n = num_env0(i);
@@ -2005,6 +2017,7 @@ public:
                 const float max_hp = gtype(i).hp;
                 static const int dir2angle[] = {0, 90, 180, 270};   // RenderGenerator.cc:148
                 for (int j = 0; j < n; j++) {
+                    if (!absorbed[i].empty() && !absorbed[i][j]) continue;
                     int h = std::max(0, int(100 * hp[j] / max_hp));
                     h = std::min(h, 100);
                     fout << ids[j] << " " << h << " " << dir2angle[dir[j] & 3] << " " << pos[2 * j] << " "
@@ -2084,11 +2097,16 @@ public:
             int ct = 1;
             for (int i = 0; i < G; i++) {
                 std::vector<int> pos = allocated ? group_pos(i) : std::vector<int>();
-                std::vector<int> ids(pos.size() / 2);
+                std::vector<int> ids(pos.size() / 2), absorbed;
                 if (!ids.empty()) MFX_CHECK(host_get(i, kGetId, ids.data(), 4));
+                if (!ids.empty() && gtype(i).can_absorb) {          // GridWorld.cc:905-906
+                    absorbed.resize(ids.size());
+                    MFX_CHECK(host_get(i, kGetAbsorbed, absorbed.data(), 4));
+                }
                 for (size_t j = 0; j < ids.size(); j++) {
                     const int x = pos[2 * j], y = pos[2 * j + 1];
                     if (x < x1 || x > x2 || y < y1 || y > y2) continue;
+                    if (!absorbed.empty() && !absorbed[j]) continue;
                     ib[4 * ct] = ids[j]; ib[4 * ct + 1] = x; ib[4 * ct + 2] = y; ib[4 * ct + 3] = i;
                     ct++;
                 }

@@ -6,7 +6,7 @@
 
 namespace mfx {
 
-enum GetWhat : int { kGetNum = 0, kGetReward = 1, kGetId = 2, kGetAlive = 3, kGetPos = 4, kGetHp = 5, kGetLastAct = 6, kGetDir = 7 };
+enum GetWhat : int { kGetNum = 0, kGetReward = 1, kGetId = 2, kGetAlive = 3, kGetPos = 4, kGetHp = 5, kGetLastAct = 6, kGetDir = 7, kGetAbsorbed = 8 };
 
 size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cells_n, int cap);
 size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap, int cap);

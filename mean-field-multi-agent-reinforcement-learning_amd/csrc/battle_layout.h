@@ -10,7 +10,8 @@
 //     hp        f32 [E][cap]
 //     next_r    f32 [E][cap]   Agent::next_reward  (GridWorld.h:248)
 //     last_r    f32 [E][cap]   Agent::last_reward
-//     last_act  u8  [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145)
+//     last_act  u8  [E][cap]   Agent::last_action  (initially n_action, GridWorld.h:145) in bits 0-6
+//                              | bit7 Agent::absorbed (GridWorld.h:196-197; can_absorb types only)
 //     op_obj    i32 [E][cap]   id of Agent::op_obj or -1
 //     meta      u8  [E][cap]   bit0 dead | bits1-2 last_op | bit3 involved (reward DSL, transient)
 //                              | bits4-5 group | bits6-7 direction ^ 3 (0 = NORTH, turn_mode)
@@ -49,7 +50,7 @@ enum : int { kEvAnd = 0, kEvOr = 1, kEvNot = 2, kEvKill = 3, kEvAt = 4, kEvIn = 
 struct TypeParams {                 // AgentType (AgentType.h:17-52), the fields the path reads
     float hp, damage, step_recover, kill_supply;
     float step_reward, kill_reward, dead_penalty, attack_penalty;
-    int attack_in_group;
+    int attack_in_group, can_absorb;           // can_absorb: Map.cc:352-356, GridWorld.cc:362/:638/:905
     int n_action, turn_base, attack_base;
     int n_move, n_attack;
     int view_w, view_h, view_x1, view_y1;      // view window relative to the agent (NORTH)
@@ -260,6 +261,11 @@ struct RolloutCtx {
     RolloutArgs ra;
     State w;
 };
+
+// last_act bit 7: the agent was absorbed (Map::do_move's can_absorb collision)
+constexpr uint32_t kLastActAbsorbed = 0x80u;
+__host__ __device__ inline uint32_t last_action(uint32_t la) { return la & 0x7Fu; }
+__host__ __device__ inline bool is_absorbed(uint32_t la) { return (la & kLastActAbsorbed) != 0u; }
 
 // meta helpers
 __host__ __device__ inline uint32_t meta_dead(uint32_t m) { return m & 1u; }

@@ -12,7 +12,9 @@
  * runs the reference build, this oracle and the HIP engine.  Supported subset = what
  * the Battle path uses: 1x1 agents, NORTH only (turn/food/goal modes
  * off), circle/sector ranges, reward rules on one binary event (attack/kill/collide)
- * between two 'any' symbols.  Anything else fails loudly (return -1 + stderr).
+ * between two 'any' symbols; plus can_absorb types (Map.cc:345-364, GridWorld.cc:357-363,
+ * :638; pinned against oracle/_ref by tests/test_absorb.py).  Anything else fails loudly
+ * (return -1 + stderr).
  *
  * Data layout is its own: agents live in an append-only pool per episode (index =
  * id), groups keep ordered id lists, the map keeps one int per cell
@@ -57,7 +59,7 @@ typedef struct {                     /* AgentType.h:17-52 (subset) */
 
 typedef struct {                     /* GridWorld.h:134-258 */
     int id, x, y, group, index;
-    bool dead;
+    bool dead, absorbed;             /* absorbed: GridWorld.h:196-197, 238 */
     float hp;
     int last_action, last_op, op_obj; /* op_obj: agent id or -1 */
     float next_reward, last_reward;
@@ -226,7 +228,6 @@ int gridworld_register_agent_type(void *game, const char *name, int n, const cha
         ORC_FAIL("invalid agent config %s", k);
     }
     if (T->width != 1 || T->length != 1) ORC_FAIL("only 1x1 agents supported");
-    if (T->can_absorb) ORC_FAIL("can_absorb unsupported");
     int parity = T->width % 2;
     if (T->view_angle >= 180) {
         if (fabs(T->view_angle - 360) > 1e-5) ORC_FAIL("angle must be 360 when > 180");
@@ -335,6 +336,7 @@ static Agent *new_agent(Env *e, int g) {
     memset(a, 0, sizeof *a);
     a->id = e->id_counter; a->group = g; a->hp = T->hp;
     a->last_action = T->n_action;                  /* GridWorld.h:145 */
+    a->absorbed = false;                           /* GridWorld.h:136 */
     a->last_op = OP_NULL; a->op_obj = -1;
     a->last_reward = 0; a->next_reward = T->step_reward;   /* init_reward() in ctor */
     return a;
@@ -422,11 +424,15 @@ int env_get_observation(void *game, int group, float **bufs) {
     float *mm = NULL;
     if (e->minimap_mode) {
         mm = calloc((size_t)VH * VW * n_group, sizeof(float));
+        /* GridWorld.cc:357-363: absorbed agents are skipped when the OBSERVING group's type can absorb
+           (the reference reads agents[0] of the observed group inside every group's loop) */
+        const bool skip = T->can_absorb;
         for (int g = 0; g < n_group; g++) {
             Group *Gi = &e->groups[g];
             size_t total = 0;
             for (int j = 0; j < Gi->n; j++) {
                 Agent *a = &e->pool[Gi->ids[j]];
+                if (skip && a->absorbed) continue;
                 mm[((a->y / scale_h) * VW + a->x / scale_w) * n_group + g] += 1.0f;
                 total++;
             }
@@ -507,7 +513,7 @@ int env_set_action(void *game, int group, const int *actions) {   /* GridWorld.c
 
 static void do_move(Env *e, Act *m) {                          /* GridWorld.cc:631-660, Map.cc:324-369 */
     Agent *a = &e->pool[m->id];
-    if (a->dead) return;
+    if (a->dead || a->absorbed) return;                         /* GridWorld.cc:638 */
     Type *T = gtype(e, a->group);
     int nx = a->x + T->move.dx[m->action], ny = a->y + T->move.dy[m->action];
     if (blank(e, nx, ny, a->id)) {
@@ -516,7 +522,20 @@ static void do_move(Env *e, Act *m) {                          /* GridWorld.cc:6
         a->x = nx; a->y = ny;
     } else if (nx >= 0 && ny >= 0 && nx + 1 < e->w && ny + 1 < e->h) {
         int v = e->cells[ny * e->w + nx];
-        if (v >= 0 && v != a->id) { a->last_op = OP_COLLIDE; a->op_obj = v; }
+        if (v >= 0 && v != a->id) {
+            Agent *o = &e->pool[v];
+            if (gtype(e, o->group)->can_absorb) {                   /* Map.cc:352-359 */
+                if (!o->absorbed) {
+                    o->absorbed = true;
+                    o->hp = o->hp * 2;
+                    a->dead = true;
+                    e->cells[a->y * e->w + a->x] = CELL_EMPTY;          /* Map::remove_agent */
+                    a->last_op = OP_COLLIDE; a->op_obj = v;
+                }
+            } else {
+                a->last_op = OP_COLLIDE; a->op_obj = v;
+            }
+        }
     }
 }
 

@@ -60,14 +60,17 @@ def test_engine_fails_loudly_without_gpu(built):
 
 
 def test_dropin_rejects_unsupported_config(built):
-    """can_absorb is the one agent attribute the engine refuses; the error surfaces at
-    register_agent_type, before any device work, so this runs without a GPU."""
+    """The reward event 'align' is the one DSL form the engine refuses (the reference reads uninitialised
+    counters for it); the rules are compiled at reset, before any device work, so
+    the refusal shows without a GPU.  can_absorb types are accepted (tests/test_absorb.py)."""
     import magent
     gw = magent.gridworld
     cfg = gw.Config()
-    cfg.set({"map_width": 10, "map_height": 10, "turn_mode": True, "food_mode": True})
-    cfg.register_agent_type("blob", {"width": 1, "length": 1, "hp": 1, "speed": 1, "can_absorb": True,
-                                     "view_range": gw.CircleRange(1), "attack_range": gw.CircleRange(1)})
-    cfg.add_group("blob")
-    with pytest.raises(magent.EngineError):
-        magent.GridWorld(cfg, lib=magent.load_library(built))
+    cfg.set({"map_width": 10, "map_height": 10})
+    t = cfg.register_agent_type("blob", {"width": 1, "length": 1, "hp": 1, "speed": 1, "can_absorb": True,
+                                         "view_range": gw.CircleRange(1), "attack_range": gw.CircleRange(1)})
+    g = cfg.add_group(t)
+    cfg.add_reward_rule(gw.Event(gw.AgentSymbol(g, "all"), "align"), receiver=gw.AgentSymbol(g, "all"), value=1.0)
+    env = magent.GridWorld(cfg, lib=magent.load_library(built))
+    with pytest.raises(magent.EngineError, match="align"):
+        env.reset()
