@@ -248,6 +248,7 @@ def run_cpu_baseline(seconds, map_size, agents, procs=None):
     steps = sum(r["agent_steps"] for r in res)
     return {"value": total, "unit": "agent-steps/s", "cores": P, "kind": res[0]["kind"],
             "per_core": total / P, "host_nproc": shown,
+            "whole_host_estimate": total / P * shown,      # per_core x every host core (linear: no shared state)
             "sample": "%d concurrent single-thread processes (OMP_NUM_THREADS=1), each %.0f s of timed env calls "
                       "of Battle %dx%d/%d (rush policy outside the clock): %d agent-steps, %d episode starts in "
                       "total; %s" % (P, seconds, map_size, map_size, agents, steps, sum(r["episodes"] for r in res),
@@ -485,6 +486,9 @@ def main():
                           ("%s, %d steps per launch" % (path, S)) if big else
                           ("fused step" if S == 1 else "fused step, %d consecutive steps per launch" % S)),
                        "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S,
+                       # agents placed per episode start vs the live agents an env-step actually carries (the
+                       # unit counts live agents; battles thin the armies, staggered episodes mix all phases)
+                       "live_agents_per_env_step": local_units / (args.steps * E),
                        "parallelism": "envs sharded one process per GPU (dp%d)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
