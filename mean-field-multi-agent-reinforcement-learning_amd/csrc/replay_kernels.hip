@@ -5,7 +5,8 @@
 // source length, MetaBuffer.sample's idx % length) into consecutive destination rows (optionally a ring:
 // MetaBuffer.append's wrap at max_len).  One launch moves every column of a batch of rows; the index
 // lists themselves (the agent grouping, the reference's np.random draws) are computed by the caller.
-// HBM-bound: 2 x the row bytes per row (read + write), coalesced dword / 16-B accesses along each row.
+// HBM-bound: 2 x the row bytes per row (read + write), coalesced dword / 16-B accesses along each row, one
+// wave per row with its loads in flight ahead of its stores (scripts/bench_replay.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -15,35 +16,90 @@
 namespace mfx {
 
 constexpr int kRowCols = 8;
+constexpr int64_t kBigRow = 512;          // columns at least this wide get a per-column vector loop
 
 struct RowCols {
     char* dst[kRowCols];
     const char* src[kRowCols];
     int64_t bytes[kRowCols];
     int n;
+    // The narrow columns (feature rows, actions, rewards, flags, mean actions) are moved together: the lanes
+    // of a wave take consecutive units of all of them at once -- unit u of column k is its
+    // (u - ustart[k])-th dword when the column's rows are 4-B aligned (ubytes 4), else its byte (ubytes 1).
+    // Wide columns (the view) have ubytes 0 and no units.
+    int ustart[kRowCols + 1];
+    int ubytes[kRowCols];
 };
 
-// Workgroup b copies rows b, b + grid, ...; each column with the widest access its alignment allows.
+// dwords [0, nd) of one row: 20 loads per lane in flight before their stores (a 4,732-B view row in one pass)
+constexpr int kCopyU4 = 20, kCopyU16 = 5;
+__device__ __forceinline__ void row_copy4(const uint32_t* __restrict__ sp, uint32_t* __restrict__ dp, int64_t nd,
+                                          int lane) {
+    for (int64_t base = 0; base < nd; base += 64 * kCopyU4) {
+        uint32_t r[kCopyU4];
+#pragma unroll
+        for (int u = 0; u < kCopyU4; ++u) {
+            const int64_t q = base + lane + 64 * u;
+            if (q < nd) r[u] = sp[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU4; ++u) {
+            const int64_t q = base + lane + 64 * u;
+            if (q < nd) dp[q] = r[u];
+        }
+    }
+}
+
+__device__ __forceinline__ void row_copy16(const uint4* __restrict__ sp, uint4* __restrict__ dp, int64_t nq, int lane) {
+    for (int64_t base = 0; base < nq; base += 64 * kCopyU16) {
+        uint4 r[kCopyU16];
+#pragma unroll
+        for (int u = 0; u < kCopyU16; ++u) {
+            const int64_t q = base + lane + 64 * u;
+            if (q < nq) r[u] = sp[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU16; ++u) {
+            const int64_t q = base + lane + 64 * u;
+            if (q < nq) dp[q] = r[u];
+        }
+    }
+}
+
+// One wave per row (four rows per workgroup): row s = idx ? idx[i] : i (modulo src_mod) of every column to
+// row d = dst_start + i (modulo dst_cap).  The narrow columns in one pass of unit loads, then each wide
+// column with its loads issued ahead of its stores -- a row is ~5 KB, so a wave keeps 2 KB in flight.
 __global__ void __launch_bounds__(256) k_rows_copy(RowCols c, const int64_t* __restrict__ idx, int64_t src_mod,
                                                    int64_t dst_start, int64_t dst_cap, int64_t n) {
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += waves) {
         int64_t s = idx ? idx[i] : i;
-        if (src_mod > 0) s = ((s % src_mod) + src_mod) % src_mod;
-        const int64_t d = dst_cap > 0 ? (dst_start + i) % dst_cap : dst_start + i;
+        if (src_mod > 0) { s %= src_mod; if (s < 0) s += src_mod; }
+        int64_t d = dst_start + i;
+        if (dst_cap > 0 && d >= dst_cap) d %= dst_cap;
+        for (int u = lane; u < c.ustart[kRowCols]; u += 64) {
+            int k = 0;
+            while (u >= c.ustart[k + 1]) ++k;
+            const int64_t b = c.bytes[k], off = u - c.ustart[k];
+            if (c.ubytes[k] == 4)
+                *reinterpret_cast<uint32_t*>(c.dst[k] + d * b + 4 * off) =
+                    *reinterpret_cast<const uint32_t*>(c.src[k] + s * b + 4 * off);
+            else
+                c.dst[k][d * b + off] = c.src[k][s * b + off];
+        }
         for (int k = 0; k < c.n; ++k) {
+            if (c.ubytes[k]) continue;
             const int64_t b = c.bytes[k];
             const char* sp = c.src[k] + s * b;
             char* dp = c.dst[k] + d * b;
-            if (((uintptr_t)sp | (uintptr_t)dp | (uintptr_t)b) % 16 == 0) {
-                const uint4* s4 = reinterpret_cast<const uint4*>(sp);
-                uint4* d4 = reinterpret_cast<uint4*>(dp);
-                for (int64_t q = threadIdx.x; q < b / 16; q += blockDim.x) d4[q] = s4[q];
-            } else if (((uintptr_t)sp | (uintptr_t)dp | (uintptr_t)b) % 4 == 0) {
-                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(sp);
-                uint32_t* d1 = reinterpret_cast<uint32_t*>(dp);
-                for (int64_t q = threadIdx.x; q < b / 4; q += blockDim.x) d1[q] = s1[q];
+            const uintptr_t al = (uintptr_t)sp | (uintptr_t)dp | (uintptr_t)b;
+            if ((al & 15) == 0) {
+                row_copy16(reinterpret_cast<const uint4*>(sp), reinterpret_cast<uint4*>(dp), b / 16, lane);
+            } else if ((al & 3) == 0) {
+                row_copy4(reinterpret_cast<const uint32_t*>(sp), reinterpret_cast<uint32_t*>(dp), b / 4, lane);
             } else {
-                for (int64_t q = threadIdx.x; q < b; q += blockDim.x) dp[q] = sp[q];
+                for (int64_t q = lane; q < b; q += 64) dp[q] = sp[q];
             }
         }
     }
@@ -68,13 +124,24 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
     if (n == 0) return 0;
     RowCols c{};
     c.n = n_cols;
+    int units = 0;
     for (int k = 0; k < n_cols; ++k) {
         if (!dst[k] || !src[k] || row_bytes[k] <= 0) return fail("rows_copy: column %d is empty", k);
         c.dst[k] = static_cast<char*>(dst[k]);
         c.src[k] = static_cast<const char*>(src[k]);
         c.bytes[k] = row_bytes[k];
+        c.ustart[k] = units;
+        if (row_bytes[k] >= kBigRow) {
+            c.ubytes[k] = 0;
+        } else {
+            const bool a4 = (((uintptr_t)dst[k] | (uintptr_t)src[k] | (uintptr_t)row_bytes[k]) & 3) == 0;
+            c.ubytes[k] = a4 ? 4 : 1;
+            units += (int)(row_bytes[k] / c.ubytes[k]);
+        }
     }
-    const int grid = (int)(n < 65536 ? n : 65536);
+    for (int k = n_cols; k <= kRowCols; ++k) c.ustart[k] = units;
+    const int64_t wgs = (n + 3) / 4;
+    const int grid = (int)(wgs < 65536 ? wgs : 65536);
     k_rows_copy<<<grid, 256, 0, (hipStream_t)stream>>>(c, d_idx, src_mod, dst_start, dst_cap, n);
     MFX_HIP(hipGetLastError());
     return 0;
