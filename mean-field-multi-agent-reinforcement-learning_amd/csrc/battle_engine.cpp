@@ -299,6 +299,7 @@ public:
         q.cells += e0 * cn; q.xy += e0 * c; q.hp += e0 * c; q.next_r += e0 * c; q.last_r += e0 * c;
         q.last_act += e0 * c; q.op_obj += e0 * c; q.meta += e0 * c; q.grp_ids += e0 * G * c;
         q.grp_n += e0 * G; q.grp_dead += e0 * G; q.grp_reward += e0 * G; q.id_counter += e0; q.rng += e0;
+        q.rid += e0 * c; q.rid_off += e0;
         q.atk += e0 * a; q.n_atk += e0; q.mov += e0 * a; q.n_mov += e0; q.done += e0;
         if (q.food) q.food += e0 * cn;
         q.idx_mark += e0;
@@ -332,7 +333,8 @@ public:
         for (void* p : {(void*)s.cells, (void*)s.xy, (void*)s.hp, (void*)s.next_r, (void*)s.last_r,
                         (void*)s.last_act, (void*)s.op_obj, (void*)s.meta, (void*)s.grp_ids, (void*)s.grp_n,
                         (void*)s.grp_dead, (void*)s.grp_reward, (void*)s.id_counter, (void*)s.rng, (void*)s.atk,
-                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)s.idx_mark, (void*)s.food, (void*)d_sort, (void*)d_gp,
+                        (void*)s.n_atk, (void*)s.mov, (void*)s.n_mov, (void*)s.done, (void*)s.idx_mark, (void*)s.food,
+                        (void*)s.rid, (void*)s.rid_off, (void*)d_sort, (void*)d_gp,
                         (void*)d_err})
             if (p) (void)hipFree(p);
         s = State{}; d_sort = nullptr; d_gp = nullptr; d_err = nullptr; allocated = false;
@@ -728,7 +730,10 @@ public:
             grow(s.xy, E, oc, nc); grow(s.hp, E, oc, nc); grow(s.next_r, E, oc, nc); grow(s.last_r, E, oc, nc);
             grow(s.last_act, E, oc, nc); grow(s.op_obj, E, oc, nc); grow(s.meta, E, oc, nc);
             grow(s.grp_ids, (size_t)E * G, oc, nc);
+            grow(s.rid, E, oc, nc);
             s.cap = nc;
+            MFX_HIP_THROW(launch_rid_fill(s, oc, stream));   // new slots: slot == id until renumbered
+            MFX_HIP_THROW(hipStreamSynchronize(stream));
         }
         if (need_actions > s.acap) {
             int na = std::max(128, s.acap);
@@ -758,7 +763,7 @@ public:
                 alloc(s.cells, (size_t)E * W * H);
                 alloc(s.grp_n, (size_t)E * G); alloc(s.grp_dead, (size_t)E * G); alloc(s.grp_reward, (size_t)E * G);
                 alloc(s.id_counter, E); alloc(s.rng, E); alloc(s.n_atk, E); alloc(s.n_mov, E); alloc(s.done, E);
-                alloc(s.idx_mark, E);
+                alloc(s.idx_mark, E); alloc(s.rid_off, E);
                 if (food) alloc(s.food, (size_t)E * W * H);
                 MFX_HIP_THROW(hipMemset(s.grp_reward, 0, sizeof(float) * E * G));   // Group ctor
                 alloc(d_gp, 1); alloc(d_err, 1);
@@ -1171,10 +1176,15 @@ public:
                 MFX_HIP_THROW(hipMemcpy(ro_walls.p, cells.data(), cells.size() * 2, hipMemcpyHostToDevice));
                 ra.wall_image = ro_walls.p;
             }
+            ra.renumber = 0;
             if (ro_big) {
                 ro_grid = E;
                 ro_sort.ensure((size_t)E * s.acap);
                 ra.big_sort = ro_sort.p;
+                // envs too large for LDS: clear_dead renumbers the slots to the list order (dense per-slot
+                // arrays); LDS-sized envs (few-env path) keep slot == id, as k_rollout assumes
+                const char* rn = getenv("MFX_RENUMBER");                   // A/B only: 0 = off
+                ra.renumber = !ro_small_e && !(rn && atoi(rn) == 0);
                 if (battle_shape(gp)) {
                     ro_mm.ensure((size_t)E * n_groups() * 169);
                     ro_info.ensure((size_t)E * s.cap);

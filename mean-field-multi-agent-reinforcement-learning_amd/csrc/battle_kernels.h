@@ -12,6 +12,7 @@ size_t observe_smem_bytes(const GameParams& gp, int g, int cells_in_lds, int cel
 size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap, int cap);
 
 hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st);
+hipError_t launch_rid_fill(const State& s, int from, hipStream_t st);   // rid[e][i] = i for i >= from
 hipError_t launch_add_agents(const GameParams* d_gp, const State& s, int group, int n, int method,
                              const int* d_xs, const int* d_ys, const int* d_dirs, int per_env_stride, hipStream_t st);
 hipError_t launch_set_goal_random(const GameParams* d_gp, const State& s, int g, hipStream_t st);

@@ -126,8 +126,12 @@ struct EnvView {
     int32_t* grp_n;        // [G]
     int32_t* grp_dead;     // [G]
     float* grp_reward;     // [G]
+    uint16_t* rid;         // [cap] reference id of each slot (HBM); null in LDS images (slot == id there)
     int cap;
 };
+
+// The reference's id of slot `id` (features, get_agent_id, policy keys)
+__device__ __forceinline__ int ref_id(const EnvView& v, int id) { return v.rid ? (int)v.rid[id] : id; }
 
 __device__ __forceinline__ EnvView global_view(const State& s, int e, int G) {
     EnvView v;
@@ -138,6 +142,7 @@ __device__ __forceinline__ EnvView global_view(const State& s, int e, int G) {
     v.grp_ids = s.grp_ids + (size_t)e * G * s.cap;
     v.food = s.food ? s.food + (size_t)e * s.cells_n : nullptr;
     v.grp_n = s.grp_n + e * G; v.grp_dead = s.grp_dead + e * G; v.grp_reward = s.grp_reward + e * G;
+    v.rid = s.rid + a;
     v.cap = s.cap;
     return v;
 }
@@ -169,6 +174,17 @@ size_t step_smem_bytes(const GameParams& gp, int cells_n, int n_ids, int acap, i
 
 hipError_t launch_reset(const GameParams* d_gp, const State& s, hipStream_t st) {
     k_reset<<<s.E, 256, 0, st>>>(d_gp, s);
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_rid_fill(State s, int from) {
+    uint16_t* r = s.rid + (size_t)blockIdx.x * s.cap;
+    for (int i = from + TID; i < s.cap; i += blockDim.x) r[i] = (uint16_t)i;
+}
+
+hipError_t launch_rid_fill(const State& s, int from, hipStream_t st) {
+    if (from >= s.cap) return hipSuccess;
+    k_rid_fill<<<s.E, 256, 0, st>>>(s, from);
     return hipGetLastError();
 }
 

@@ -4,8 +4,11 @@
 // agent types, reward rules).  All per-env state is struct-of-arrays in HBM with a fixed
 // per-env stride, so a workgroup that owns env e touches only its own slabs:
 //
-//   cells     u16 [E][H*W]    0xFFFF empty, 0xFFFE wall, else the occupying agent's id
-//   agents (indexed by id, ids are dense 0..id_counter-1 within an episode, GridWorld.cc:184)
+//   cells     u16 [E][H*W]    0xFFFF empty, 0xFFFE wall, else the occupying agent's slot
+//   agents (indexed by slot, slots are dense 0..id_counter-1).  A slot is the agent's id
+//   (GridWorld.cc:184) until the large-env rollout renumbers the slots to the list order at a
+//   clear_dead (clear_dead_renumber, battle/rollout_big.inc); the id itself is always rid[slot]
+//     rid       u16 [E][cap]   the reference's agent id of the slot (features, get_agent_id, keys)
 //     xy        u32 [E][cap]   x | y << 16
 //     hp        f32 [E][cap]
 //     next_r    f32 [E][cap]   Agent::next_reward  (GridWorld.h:248)
@@ -18,7 +21,8 @@
 //   groups
 //     grp_ids   u16 [E][G][cap] the ordered agent vector of each group (Group::agents)
 //     grp_n, grp_dead i32 [E][G];  grp_reward f32 [E][G]
-//   id_counter i32 [E], rng u32 [E] (minstd_rand0 state, GridWorld.h:106)
+//   id_counter i32 [E] slots in use, rid_off i32 [E] the reference's id_counter minus id_counter
+//   (0 unless renumbered), rng u32 [E] (minstd_rand0 state, GridWorld.h:106)
 //   pending actions since the last step (GridWorld::set_action, GridWorld.cc:430-496)
 //     atk u32 [E][acap] = id << 8 | attack index      n_atk i32 [E]
 //     mov u32 [E][acap] = id << 16 | move index << 8 | bucket (0xFF = boundary buffer)
@@ -124,7 +128,9 @@ struct State {                      // device pointers; every array is [E][strid
     int32_t* grp_n;                 // [E][G]
     int32_t* grp_dead;              // [E][G]
     float* grp_reward;              // [E][G]
-    int32_t* id_counter;            // [E]
+    int32_t* id_counter;            // [E] slots in use
+    uint16_t* rid;                  // [E][cap] reference id of each slot
+    int32_t* rid_off;               // [E] next id add_agents hands out (GridWorld::id_counter) - id_counter
     uint32_t* rng;                  // [E]
     uint32_t* atk;                  // [E][acap]
     int32_t* n_atk;                 // [E]
@@ -221,6 +227,8 @@ struct RolloutArgs {
                                     // followed by int32 [grp_n[kMaxGroups], id_counter]
     int env_base;                   // index of env 0 of this (sub-)batch in the whole batch (policy keys)
     uint32_t* big_sort;             // large envs: [E][acap] band-ordered move buffer of k_rollout_big
+    int renumber;                   // large envs: clear_dead renumbers the slots to the list order, so
+                                    //   the per-slot arrays of the live agents stay dense (rid keeps ids)
     float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and
     uint32_t* obs_info;             //   [E][cap] packed hp/max | group << 31 of the NEXT observation,
                                     //   computed once per env at the end of the step (obs_prep_env)

@@ -437,6 +437,93 @@ def test_rollout_large_env_staggered_many_envs_matches_oracle():
     assert restarts >= E
 
 
+def test_rollout_large_env_renumbered_slots_per_call():
+    """Large envs renumber their slots to the list order at every rollout clear_dead
+    (clear_dead_renumber): after kills a slot is no longer the agent's id, which lives on in rid, and the
+    reference's id_counter runs ahead of the slots in use (rid_off).  Per-call calls on that state must
+    still answer as the reference does: get_agent_id (batched getter and the drop-in's env-0 record),
+    add_agents (new agents take the reference's next ids), a per-call observation (features embed the id),
+    a per-call step with attacks and clear_dead -- and rollout launches after them (a re-seed) continue
+    the oracle replay bit for bit."""
+    import torch
+    from mfrl_amd.battle import BattleBatch, GET_HP, GET_ID, GET_POS, GET_REWARD
+    E, M, n_side, T, T2, seed, eps = 2, 200, 1250, 24, 12, 5, 0.3
+    placement = bd.block_positions(M, n_side)
+    eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
+    eng.rollout_init(placement, max_steps=400, eps=eps, seed=seed, stagger=False)
+    assert eng.rollout_path() == "k_rollout_bigq"
+    chk = rck.RolloutChecker(eng, M, placement, list(range(E)), 400, False, seed, eps)
+    eng.rollout_step(T)
+    bad = chk.check(T)
+    assert not bad, bad[:8]
+    reps = chk.replays
+    assert all(sum(rep.oracle.get_num(h) for h in rep.h) < 2 * n_side for rep in reps)   # kills: renumbered
+    rc, VF, F = eng.rowcap, 13 * 13 * 7, 34
+    H = eng.handles
+
+    def per_group(what, dt, w=1):
+        out = []
+        for g in range(2):
+            buf = torch.empty((E, rc, w), dtype=dt, device="cuda")
+            eng.get(g, what, buf, rc)
+            out.append(buf)
+        eng.sync()
+        return [x.cpu().numpy() for x in out]
+
+    def compare_state(tag):
+        ids, pos, hp = per_group(GET_ID, torch.int32), per_group(GET_POS, torch.int32, 2), per_group(GET_HP, torch.float32)
+        for e, rep in enumerate(reps):
+            for g in range(2):
+                want = rep.oracle.get_agent_id(rep.h[g])
+                m = len(want)
+                assert ids[g][e, :m, 0].tobytes() == want.tobytes(), (tag, e, g, "ids")
+                assert pos[g][e, :m].tobytes() == rep.oracle.get_pos(rep.h[g]).tobytes(), (tag, e, g, "pos")
+                got_hp = rep.oracle._info_array(rep.h[g], b"hp", (m,), np.float32)
+                assert hp[g][e, :m, 0].tobytes() == got_hp.tobytes(), (tag, e, g, "hp")
+        for g in range(2):      # the drop-in's env-0 record (k_get_env0)
+            assert eng.env.get_agent_id(H[g]).tobytes() == reps[0].oracle.get_agent_id(reps[0].h[g]).tobytes(), (tag, g)
+
+    compare_state("after the rollout")
+    eng.env.add_agents(H[0], method="random", n=7)
+    for rep in reps:
+        rep.oracle.add_agents(rep.h[0], method="random", n=7)
+    compare_state("after add_agents")
+    assert int(reps[0].oracle.get_agent_id(reps[0].h[0])[-1]) == 2 * n_side + 6      # the reference's next ids
+    view = [torch.empty(E * rc * VF, dtype=torch.float32, device="cuda") for _ in range(2)]
+    feat = [torch.empty(E * rc * F, dtype=torch.float32, device="cuda") for _ in range(2)]
+    for g in range(2):
+        eng.observe(g, view[g], feat[g], rc)
+    eng.sync()
+    rng = np.random.RandomState(3)
+    acts = torch.zeros((2, E, rc), dtype=torch.int32)
+    for e, rep in enumerate(reps):
+        for g in range(2):
+            v, f = rep.oracle.get_observation(rep.h[g])
+            n = len(v)
+            assert view[g].cpu().numpy().reshape(E, rc, VF)[e, :n].tobytes() == v.reshape(n, VF).tobytes(), (e, g)
+            assert feat[g].cpu().numpy().reshape(E, rc, F)[e, :n].tobytes() == f.tobytes(), (e, g)
+            a = rng.randint(0, 21, size=n).astype(np.int32)
+            acts[g, e, :n] = torch.from_numpy(a)
+            rep.oracle.set_action(rep.h[g], a)
+    for g in range(2):
+        eng.set_action(g, acts[g].cuda().contiguous(), rc)
+    eng.step()
+    for rep in reps:
+        rep.oracle.step()
+    rew = per_group(GET_REWARD, torch.float32)
+    for e, rep in enumerate(reps):
+        for g in range(2):
+            rw = rep.oracle.get_reward(rep.h[g])
+            assert rew[g][e, :len(rw), 0].tobytes() == rw.tobytes(), (e, g, "reward")
+    eng.clear_dead()
+    for rep in reps:
+        rep.oracle.clear_dead()
+    compare_state("after a per-call step")
+    eng.rollout_step(T2)                             # re-seed; the replays continue on the changed oracles
+    bad = chk.check(T + T2)
+    assert not bad, bad[:8]
+
+
 def test_rollout_large_env_queue_matches_pipeline(monkeypatch):
     """The queue-driven large-env kernel (k_rollout_bigq: observation items and the steps they gate in
     one launch, several steps of every env per launch, items filed inside the launch) against the
