@@ -1183,8 +1183,8 @@ public:
                 ra.big_sort = ro_sort.p;
                 // envs too large for LDS: clear_dead renumbers the slots to the list order (dense per-slot
                 // arrays); LDS-sized envs (few-env path) keep slot == id, as k_rollout assumes
-                const char* rn = getenv("MFX_RENUMBER");                   // A/B only: 0 = off
-                ra.renumber = !ro_small_e && !(rn && atoi(rn) == 0);
+                const char* rn = getenv("MFX_RENUMBER");       // A/B only: 0 = off, 2 = no identity fast path
+                ra.renumber = ro_small_e ? 0 : (rn ? std::min(std::max(atoi(rn), 0), 2) : 1);
                 if (battle_shape(gp)) {
                     ro_mm.ensure((size_t)E * n_groups() * 169);
                     ro_info.ensure((size_t)E * s.cap);

@@ -228,7 +228,8 @@ struct RolloutArgs {
     int env_base;                   // index of env 0 of this (sub-)batch in the whole batch (policy keys)
     uint32_t* big_sort;             // large envs: [E][acap] band-ordered move buffer of k_rollout_big
     int renumber;                   // large envs: clear_dead renumbers the slots to the list order, so
-                                    //   the per-slot arrays of the live agents stay dense (rid keeps ids)
+                                    //   the per-slot arrays of the live agents stay dense (rid keeps ids);
+                                    //   2: without the identity fast path (A/B only)
     float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and
     uint32_t* obs_info;             //   [E][cap] packed hp/max | group << 31 of the NEXT observation,
                                     //   computed once per env at the end of the step (obs_prep_env)
