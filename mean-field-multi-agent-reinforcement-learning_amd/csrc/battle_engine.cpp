@@ -1177,6 +1177,7 @@ public:
                 ra.wall_image = ro_walls.p;
             }
             ra.renumber = 0;
+            ra.lds_step = 0;
             if (ro_big) {
                 ro_grid = E;
                 ro_sort.ensure((size_t)E * s.acap);
@@ -1185,6 +1186,9 @@ public:
                 // arrays); LDS-sized envs (few-env path) keep slot == id, as k_rollout assumes
                 const char* rn = getenv("MFX_RENUMBER");       // A/B only: 0 = off, 2 = no identity fast path
                 ra.renumber = ro_small_e ? 0 : (rn ? std::min(std::max(atoi(rn), 0), 2) : 1);
+                // few LDS-sized envs: each env is staged in LDS for its step (big_env_step)
+                const char* ls = getenv("MFX_LDS_STEP");                   // A/B only: 0 = the step in HBM
+                ra.lds_step = ro_small_e && !(ls && atoi(ls) == 0);
                 if (battle_shape(gp)) {
                     ro_mm.ensure((size_t)E * n_groups() * 169);
                     ro_info.ensure((size_t)E * s.cap);
@@ -1209,8 +1213,8 @@ public:
                     const int Rq = rv && atoi(rv) > 0 ? atoi(rv) : (ro_small_e ? kSmallERows : kBigqRows);
                     const int chunks = (ra.rowcap + Rq - 1) / Rq;
                     ro_bigq = ro_bigq_want && E <= 8192 && chunks <= 64 && n_groups() == 2 &&
-                              bigq_smem_bytes(gp, s.cap, s.acap, Rq) <= 160 * 1024;
-                    if (ro_bigq) MFX_HIP_THROW(bigq_grid(gp, s.cap, s.acap, Rq, &ro_q_grid));
+                              bigq_smem_bytes(gp, s.cap, s.acap, Rq, ra.lds_step) <= 160 * 1024;
+                    if (ro_bigq) MFX_HIP_THROW(bigq_grid(gp, s.cap, s.acap, Rq, ra.lds_step, &ro_q_grid));
                     ro_bigq = ro_bigq && ro_q_grid > 0;          // (0: not one SPX device of 8 XCDs)
                     if (ro_bigq) {
                         // per list and parity: one filing per env and step of a launch (<= 64 steps)
@@ -1312,7 +1316,7 @@ public:
                 ro_qdone += (uint32_t)E * (uint32_t)k;
                 MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, ro_qpar,
                                             qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
-                                            stream));
+                                            ra.lds_step, stream));
                 ro_qpar ^= 1;
                 ro_qlaunch++;
                 ro_launch++;
@@ -1346,7 +1350,7 @@ public:
                             MFX_HIP(launch_observe(gp, d_gp, q, g, qa.rowcap, qa.view[g], qa.feat[g], qa.rowcap,
                                                    ro_str[k]));
                     }
-                    MFX_HIP(launch_rollout_big(gp, d_gp, q, ro_sub_ctx.p + k, ra.step_index, ro_str[k]));
+                    MFX_HIP(launch_rollout_big(gp, d_gp, q, ro_sub_ctx.p + k, ra.step_index, ra.lds_step, ro_str[k]));
                 }
                 ro_launch++;
                 ra.step_index++;
@@ -1440,7 +1444,7 @@ public:
     int rollout_info(int* grid, int* lds_bytes) {
         if (!rollout_ready) return fail("rollout_info before rollout_init");
         *grid = ro_grid;
-        *lds_bytes = (int)(ro_big ? big_step_smem_bytes(gp, s.cap, s.acap, true)
+        *lds_bytes = (int)(ro_big ? big_step_smem_bytes(gp, s.cap, s.acap, true, ra.lds_step)
                                   : rollout_smem_bytes(gp, s.cells_n, s.cap, s.acap, ra.rowcap));
         return 0;
     }

@@ -294,21 +294,21 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
 }
 
 hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
-                              uint32_t step_index, hipStream_t st) {
-    const size_t smem = big_step_smem_bytes(gp, s.cap, s.acap, true);
+                              uint32_t step_index, bool lds_env, hipStream_t st) {
+    const size_t smem = big_step_smem_bytes(gp, s.cap, s.acap, true, lds_env);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     k_rollout_big<<<s.E, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, step_index);
     return hipGetLastError();
 }
 
-size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows) {
-    const size_t a = big_step_smem_bytes(gp, cap, acap, true);
+size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows, bool lds_env) {
+    const size_t a = big_step_smem_bytes(gp, cap, acap, true, lds_env);
     const size_t b = obs_smem_core(gp, 0, 0, rows, obs_stage_floats(gp, 0, true, kBigRolloutThreads), true);
     return a > b ? a : b;
 }
 
-hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, int* grid) {
-    const size_t smem = bigq_smem_bytes(gp, cap, acap, rows);
+hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, bool lds_env, int* grid) {
+    const size_t smem = bigq_smem_bytes(gp, cap, acap, rows, lds_env);
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t err = hipGetDevice(&dev);
     if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -329,8 +329,8 @@ hipError_t launch_bigq_seed(const GameParams* d_gp, const State& s, const Rollou
 
 hipError_t launch_rollout_bigq(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                                int rows, uint32_t si0, int n_sub, int par, uint32_t tag_cur, uint32_t tag_next,
-                               int32_t done_target, int grid, hipStream_t st) {
-    const size_t smem = bigq_smem_bytes(gp, s.cap, s.acap, rows);
+                               int32_t done_target, int grid, bool lds_env, hipStream_t st) {
+    const size_t smem = bigq_smem_bytes(gp, s.cap, s.acap, rows, lds_env);
     if (smem > 160 * 1024 || grid < 1 || n_sub < 1) return hipErrorInvalidValue;
     k_rollout_bigq<<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
                                                           done_target);

@@ -230,6 +230,8 @@ struct RolloutArgs {
     int renumber;                   // large envs: clear_dead renumbers the slots to the list order, so
                                     //   the per-slot arrays of the live agents stay dense (rid keeps ids);
                                     //   2: without the identity fast path (A/B only)
+    int lds_step;                   // few LDS-sized envs on the queue kernel: big_env_step stages the env in
+                                    //   LDS for the step and writes it back (BigLayout::img)
     float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and
     uint32_t* obs_info;             //   [E][cap] packed hp/max | group << 31 of the NEXT observation,
                                     //   computed once per env at the end of the step (obs_prep_env)
