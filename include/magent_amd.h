@@ -130,6 +130,9 @@ int mfx_battle_rollout_check(void *game);
 /* The kernels rollout_step runs: 0 k_rollout, 1 k_rollout_obs + k_rollout (pipeline), 2 k_observe_items +
  * k_rollout_big (large-env pipeline), 3 k_rollout_bigq. */
 int mfx_battle_rollout_path(void *game, int *path);
+/* Lanes over which the rollout sums a group's rewards of an env with n_agents agents: the summation order of
+ * the episode returns (64: one wave, 256 / 512: a workgroup's lane-strided partials, then wave sums). */
+int mfx_battle_rollout_sum_lanes(void *game, int n_agents, int *lanes);
 /* A learned policy in the loop (the fused k_rollout path: batches of LDS-sized envs larger than the few-env
  * threshold): mode 2 writes every env's observation into the rollout buffers; mode 1 takes the actions in
  * the rollout's action buffer (a policy forward on that observation, e.g. mfx_qnet_act_rollout), runs

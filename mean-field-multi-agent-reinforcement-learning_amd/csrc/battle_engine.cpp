@@ -1441,6 +1441,15 @@ public:
         return ro_pipe ? 1 : 0;
     }
 
+    // Lanes over which the rollout sums a group's rewards of an env with n agents (the order the episode
+    // returns follow): k_rollout's wave 0 up to 64 agents, else its workgroup; the step of the large-env
+    // and few-env paths (big_env_step) 512 lanes.
+    int rollout_sum_lanes(int n) const {
+        if (!rollout_ready) return -1;
+        if (ro_big) return 512;                       // kBigRolloutThreads (battle/rollout_big.inc)
+        return n <= 64 ? 64 : 256;
+    }
+
     int rollout_info(int* grid, int* lds_bytes) {
         if (!rollout_ready) return fail("rollout_info before rollout_init");
         *grid = ro_grid;
@@ -2323,6 +2332,15 @@ MFX_API int mfx_battle_rollout_path(void* game, int* path) {
     const int p = MFX_ENV(game)->rollout_path();
     if (p < 0) return mfx::fail("rollout_path before rollout_init");
     *path = p;
+    return 0;
+}
+
+// Lanes over which the rollout sums a group's rewards of an env with n_agents agents (the summation order
+// the episode returns follow; the oracle replay restates it).
+MFX_API int mfx_battle_rollout_sum_lanes(void* game, int n_agents, int* lanes) {
+    const int l = MFX_ENV(game)->rollout_sum_lanes(n_agents);
+    if (l < 0) return mfx::fail("rollout_sum_lanes before rollout_init");
+    *lanes = l;
     return 0;
 }
 

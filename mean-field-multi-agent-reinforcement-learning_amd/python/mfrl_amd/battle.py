@@ -33,7 +33,7 @@ class BattleBatch:
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
                    "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check", "mfx_battle_rollout_path",
-                   "mfx_battle_rollout_policy_step"):
+                   "mfx_battle_rollout_policy_step", "mfx_battle_rollout_sum_lanes"):
             try:
                 getattr(self._dll, fn).restype = ctypes.c_int
             except AttributeError:          # an older build of the library (A/B runs)
@@ -133,6 +133,14 @@ class BattleBatch:
         p = ctypes.c_int()
         self._check(self._dll.mfx_battle_rollout_path(self.game, ctypes.byref(p)), "rollout_path")
         return self.PATHS[p.value]
+
+    def rollout_sum_lanes(self, n_agents):
+        """Lanes over which the rollout sums a group's rewards of an env with n_agents agents (the order
+        of the episode-return sums; the oracle replay restates it)."""
+        p = ctypes.c_int()
+        self._check(self._dll.mfx_battle_rollout_sum_lanes(self.game, int(n_agents), ctypes.byref(p)),
+                    "rollout_sum_lanes")
+        return p.value
 
     def rollout_substeps(self, n_sub):
         """Consecutive steps of every env per k_rollout launch (results do not depend on it)."""

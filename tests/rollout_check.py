@@ -93,9 +93,12 @@ def device_sum(r, lanes):
     return tot
 
 
-def team_lanes(path, n_total):
+def team_lanes(path, n_total, lanes=None):
     """Lanes that sum an env's rewards: k_rollout's wave 0 alone for <= 64 agents, else its 256-lane
-    workgroup; the large-env step (k_rollout_big, k_rollout_bigq) always 512 lanes."""
+    workgroup; the large-env and few-env step (k_rollout_big, k_rollout_bigq) 512 lanes.  lanes: the engine's
+    own (lanes for <= 64 agents, lanes above), from BattleBatch.rollout_sum_lanes, which takes precedence."""
+    if lanes is not None:
+        return lanes[0] if n_total <= 64 else lanes[1]
     if path in ("k_rollout", "k_rollout_obs+k_rollout"):
         return 64 if n_total <= 64 else 256
     return 512
@@ -104,10 +107,11 @@ def team_lanes(path, n_total):
 class EnvReplay:
     """Env `env` of a batch of E, replayed on the C oracle step by step from rollout_init."""
 
-    def __init__(self, map_size, placement, env, E, max_steps, stagger, seed, eps, path, lib=None):
+    def __init__(self, map_size, placement, env, E, max_steps, stagger, seed, eps, path, lib=None, lanes=None):
         self.oracle, self.h = common.battle_env(lib or common.ORACLE_LIB, map_size)
         self.placement = placement
         self.e, self.seed, self.eps, self.path, self.max_steps = env, seed, eps, path, max_steps
+        self.lanes = lanes
         self.G = len(self.h)
         self.n_action = self.oracle.get_action_space(self.h[0])[0]
         self.attack_base, self.v2a = self.oracle.get_view2attack(self.h[0])
@@ -141,7 +145,7 @@ class EnvReplay:
         done = o.step()
         rew = [o.get_reward(h[g]) for g in range(self.G)]
         kills = sum(int((~o.get_alive(h[g])).sum()) for g in range(self.G))
-        lanes = team_lanes(self.path, sum(n))
+        lanes = team_lanes(self.path, sum(n), self.lanes)
         for g in range(self.G):
             self.ep_return[g] = np.float32(self.ep_return[g] + device_sum(rew[g], lanes))
         self.stats[3] += float(kills)
@@ -267,8 +271,9 @@ class RolloutChecker:
     def __init__(self, eng, map_size, placement, envs, max_steps, stagger, seed, eps, lib=None):
         self.eng, self.envs = eng, list(envs)
         self.path = eng.rollout_path()
-        self.replays = [EnvReplay(map_size, placement, e, eng.n_envs, max_steps, stagger, seed, eps, self.path, lib=lib)
-                        for e in self.envs]
+        lanes = (eng.rollout_sum_lanes(64), eng.rollout_sum_lanes(65))
+        self.replays = [EnvReplay(map_size, placement, e, eng.n_envs, max_steps, stagger, seed, eps, self.path, lib=lib,
+                                  lanes=lanes) for e in self.envs]
 
     def check(self, T):
         eng = self.eng
