@@ -117,26 +117,16 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
         }
         qwave_sync();
         fetch(i + step);
-        // ---- Conv1: 8 position tiles (121 of 128 rows) x 2 channel tiles, K 64.  The next tile's 16 A
-        // operands are read from LDS while this tile's 32 MFMAs issue (left to itself the compiler waits on
-        // each read right before its two MFMAs: the LDS latency exposed 16 times per tile)
-        float a1[16], a1n[16];
-        auto conv1_load = [&](int mt, float* dst) {
+        // ---- Conv1: 8 position tiles (121 of 128 rows) x 2 channel tiles, K 64
+        for (int mt = 0; mt < 8; ++mt) {
             const int pa = min(mt * 16 + c, kQC1 * kQC1 - 1);
             const int vb = ((pa / kQC1) * kQVW + pa % kQC1) * kQNC;
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk) dst[kk] = vs[vb + koff[kk]];
-        };
-        conv1_load(0, a1);
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-            if (mt + 1 < 8) conv1_load(mt + 1, a1n);
-            __builtin_amdgcn_sched_barrier(0);           // keep the prefetch above the MFMAs
             f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) {
-                d0 = mfma4(a1[kk], b1r[kk][0], d0);
-                d1 = mfma4(a1[kk], b1r[kk][1], d1);
+                const float a = vs[vb + koff[kk]];
+                d0 = mfma4(a, b1r[kk][0], d0);
+                d1 = mfma4(a, b1r[kk][1], d1);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -146,8 +136,6 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
                     c1[pos * kQC1Ld + 16 + c] = fmaxf(d1[r] + bias1b, 0.f);
                 }
             }
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk) a1[kk] = a1n[kk];
         }
         qwave_sync();
         // ---- Conv2: 6 position tiles (81 of 96 rows) x 2 channel tiles, K 288 (72 k-steps); im2col
@@ -161,28 +149,17 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
             acc[mt][0] = {0.f, 0.f, 0.f, 0.f};
             acc[mt][1] = {0.f, 0.f, 0.f, 0.f};
         }
-        // k-step kk + 1's eight LDS operands are read while k-step kk's 12 MFMAs issue
-        float a2[6], a2n[6], b2[2], b2n[2];
-        auto conv2_load = [&](int kk, float* a, float* b) {
-            const int so = ((kk / 24) * kQC1 + (kk / 8) % 3) * kQC1Ld + (kk % 8) * 4;
-            b[0] = w2[(kk * 4 + h) * kQW2Ld + c];
-            b[1] = w2[(kk * 4 + h) * kQW2Ld + 16 + c];
-#pragma unroll
-            for (int mt = 0; mt < 6; ++mt) a[mt] = c1[cb[mt] + so];
-        };
-        conv2_load(0, a2, b2);
 #pragma unroll 4
-        for (int kk = 0; kk < kQK2 / 4; ++kk) {
-            if (kk + 1 < kQK2 / 4) conv2_load(kk + 1, a2n, b2n);
-            __builtin_amdgcn_sched_barrier(0);
+        for (int kk = 0; kk < kQK2 / 4; ++kk) {              // (unrolled: the next k-steps' LDS reads issue
+                                                             //  under this one's MFMAs)
+            const int so = ((kk / 24) * kQC1 + (kk / 8) % 3) * kQC1Ld + (kk % 8) * 4;
+            const float b0 = w2[(kk * 4 + h) * kQW2Ld + c], b1 = w2[(kk * 4 + h) * kQW2Ld + 16 + c];
 #pragma unroll
             for (int mt = 0; mt < 6; ++mt) {
-                acc[mt][0] = mfma4(a2[mt], b2[0], acc[mt][0]);
-                acc[mt][1] = mfma4(a2[mt], b2[1], acc[mt][1]);
+                const float a = c1[cb[mt] + so];
+                acc[mt][0] = mfma4(a, b0, acc[mt][0]);
+                acc[mt][1] = mfma4(a, b1, acc[mt][1]);
             }
-#pragma unroll
-            for (int mt = 0; mt < 6; ++mt) a2[mt] = a2n[mt];
-            b2[0] = b2n[0]; b2[1] = b2n[1];
         }
         float* o = out + (size_t)i * kQFlat;
 #pragma unroll
