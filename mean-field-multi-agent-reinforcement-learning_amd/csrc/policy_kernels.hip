@@ -61,9 +61,12 @@ __device__ __forceinline__ void qwave_sync() {
 // strides chosen for the banks (ds_read_b32: 32 banks per half-wave of 16 rows x 2 k): w2's 48 (16 mod
 // 32) puts the two k rows of a half-wave on different banks, conv1's 34 (2 mod 32) the 16 positions.
 constexpr int kQConvWaves = 4;
-constexpr int kQW2Ld = 48, kQC1Ld = 34;
+// Conv2's weights transposed, w2t [32 channels][288 + 4] (k contiguous per channel), and conv1's output rows
+// at a 36-float stride: both 16-B aligned, so a lane reads its 8 consecutive k of one (ky, kx) block with two
+// ds_read_b128 (the k order inside a block is permuted to make them consecutive: see Conv2 below).
+constexpr int kQW2tLd = kQK2 + 4, kQC1Ld = 36;
 constexpr int kQViewLds = 1184, kQC1Lds = kQC1 * kQC1 * kQC1Ld;
-constexpr size_t kQConvSmem = (size_t)(kQK1 * kQCh + kQK2 * kQW2Ld + kQConvWaves * (kQViewLds + kQC1Lds)) * 4;
+constexpr size_t kQConvSmem = (size_t)(kQK1 * kQCh + kQCh * kQW2tLd + kQConvWaves * (kQViewLds + kQC1Lds)) * 4;
 
 // Offset of im2col column k (ky, kx, ci) in the staged 13 x 13 x 7 view; the pad column 63 reads
 // element 0 against a zero weight row.
@@ -80,10 +83,10 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
     float* w1 = qsm;
     float* w2 = w1 + kQK1 * kQCh;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
-    float* vs = w2 + kQK2 * kQW2Ld + wid * (kQViewLds + kQC1Lds);
+    float* vs = w2 + kQCh * kQW2tLd + wid * (kQViewLds + kQC1Lds);
     float* c1 = vs + kQViewLds;
     for (int i = threadIdx.x; i < kQK1 * kQCh; i += blockDim.x) w1[i] = p.w1[i];
-    for (int i = threadIdx.x; i < kQK2 * kQCh; i += blockDim.x) w2[(i / kQCh) * kQW2Ld + i % kQCh] = p.w2[i];
+    for (int i = threadIdx.x; i < kQK2 * kQCh; i += blockDim.x) w2[(i % kQCh) * kQW2tLd + i / kQCh] = p.w2[i];
     __syncthreads();
     // conv1's B operands for all 16 k-steps stay in registers, so do the lane's im2col offsets
     float b1r[16][2];
@@ -138,29 +141,64 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
             }
         }
         qwave_sync();
-        // ---- Conv2: 6 position tiles (81 of 96 rows) x 2 channel tiles, K 288 (72 k-steps); im2col
-        // column k = 4 kk + h is (ky, kx, ci) = (kk / 24, kk / 8 % 3, 4 (kk % 8) + h)
+        // ---- Conv2: 6 position tiles (81 of 96 rows) x 2 channel tiles, K 288 = 9 (ky, kx) blocks x 32 ci.
+        // Inside block b the 8 k-steps j give lane group h the channels ci = 8 h + j (any order of k is the same
+        // sum up to rounding), so a lane's A operands of a block (per tile) and B operands (per channel tile) are
+        // 8 consecutive floats: 16 ds_read_b128 per block for 96 MFMAs, the next block's in flight meanwhile.
         f32x4 acc[6][2];
         int cb[6];
 #pragma unroll
         for (int mt = 0; mt < 6; ++mt) {
             const int pa = min(mt * 16 + c, kQC2 * kQC2 - 1);
-            cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQC1Ld + h;
+            cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQC1Ld + 8 * h;
             acc[mt][0] = {0.f, 0.f, 0.f, 0.f};
             acc[mt][1] = {0.f, 0.f, 0.f, 0.f};
         }
-#pragma unroll 4
-        for (int kk = 0; kk < kQK2 / 4; ++kk) {              // (unrolled: the next k-steps' LDS reads issue
-                                                             //  under this one's MFMAs)
-            const int so = ((kk / 24) * kQC1 + (kk / 8) % 3) * kQC1Ld + (kk % 8) * 4;
-            const float b0 = w2[(kk * 4 + h) * kQW2Ld + c], b1 = w2[(kk * 4 + h) * kQW2Ld + 16 + c];
+        typedef float f32x8 __attribute__((ext_vector_type(8)));
+        // Each block's 16 reads go out in two parts under the previous block's MFMAs (10 before its first half,
+        // 6 before its second), so no wait ever has to name more than 15 newer LDS operations (lgkmcnt's range).
+        f32x8 p0[6], q0[2], p1[6], q1[2];
+        auto conv2_part = [&](int b, f32x8* a, f32x8* w, int part) {
+            const int ky = b / 3, kx = b % 3;
+            const int so = (ky * kQC1 + kx) * kQC1Ld;
+            if (part == 0) {
 #pragma unroll
-            for (int mt = 0; mt < 6; ++mt) {
-                const float a = c1[cb[mt] + so];
-                acc[mt][0] = mfma4(a, b0, acc[mt][0]);
-                acc[mt][1] = mfma4(a, b1, acc[mt][1]);
+                for (int q = 0; q < 2; ++q) w[q] = *reinterpret_cast<const f32x8*>(w2 + (16 * q + c) * kQW2tLd + b * 32 + 8 * h);
+#pragma unroll
+                for (int mt = 0; mt < 3; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
+            } else {
+#pragma unroll
+                for (int mt = 3; mt < 6; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
             }
+        };
+        auto conv2_half = [&](const f32x8* a, const f32x8* w, int j0) {
+#pragma unroll
+            for (int j = j0; j < j0 + 4; ++j)
+#pragma unroll
+                for (int mt = 0; mt < 6; ++mt) {
+                    acc[mt][0] = mfma4(a[mt][j], w[0][j], acc[mt][0]);
+                    acc[mt][1] = mfma4(a[mt][j], w[1][j], acc[mt][1]);
+                }
+        };
+        // one block's MFMAs with the next block's reads interleaved (nb < 0: none)
+        auto conv2_step = [&](const f32x8* a, const f32x8* w, f32x8* na, f32x8* nw, int nb) {
+            if (nb >= 0) conv2_part(nb, na, nw, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            conv2_half(a, w, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (nb >= 0) conv2_part(nb, na, nw, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            conv2_half(a, w, 4);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        conv2_part(0, p0, q0, 0);
+        conv2_part(0, p0, q0, 1);
+#pragma unroll 1
+        for (int b = 0; b < 8; b += 2) {                 // ping-pong: block b in (p0, q0), b + 1 in (p1, q1)
+            conv2_step(p0, q0, p1, q1, b + 1);
+            conv2_step(p1, q1, p0, q0, b + 2);
         }
+        conv2_step(p0, q0, p1, q1, -1);                  // block 8
         float* o = out + (size_t)i * kQFlat;
 #pragma unroll
         for (int mt = 0; mt < 6; ++mt)
