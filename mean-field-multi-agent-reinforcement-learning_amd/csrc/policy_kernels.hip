@@ -14,7 +14,8 @@
 // (157 TF/s -> ~4.6e7 agents/s for the whole chip).  Two kernels:
 //   k_qnet_conv  one wave per agent: the view staged in LDS, Conv1 as an implicit GEMM over 121
 //                positions x 32 channels x K 63 (padded to 64), its output kept in LDS, Conv2 as an
-//                implicit GEMM over 81 positions x 32 x K 288; the 2,592 activations to HBM (10 KB/agent)
+//                implicit GEMM over 81 positions x 32 x K 288 (16-B operand reads, k permuted inside each
+//                (ky, kx) block); the 2,592 activations to HBM (10 KB/agent)
 //   k_qnet_head  four waves x 16 agents per workgroup: every layer transposed (weights as the A operand),
 //                so each layer's accumulators are the next layer's B operand in registers; the weight
 //                chunks staged in LDS and shared by the four waves; the Q values and the argmax
@@ -57,9 +58,8 @@ __device__ __forceinline__ void qwave_sync() {
 }
 
 // ------------------------------------------------------------------------------------------ conv
-// LDS: w1 [64][32], w2 [288][48] (shared), per wave the view [1,184] and conv1's output [121][34].  Row
-// strides chosen for the banks (ds_read_b32: 32 banks per half-wave of 16 rows x 2 k): w2's 48 (16 mod
-// 32) puts the two k rows of a half-wave on different banks, conv1's 34 (2 mod 32) the 16 positions.
+// LDS: w1 [64][32] and Conv2's weights transposed, w2t [32][292] (shared), per wave the view [1,184] and
+// conv1's output [121][36] (134 KB per 4-wave workgroup).
 constexpr int kQConvWaves = 4;
 // Conv2's weights transposed, w2t [32 channels][288 + 4] (k contiguous per channel), and conv1's output rows
 // at a 36-float stride: both 16-B aligned, so a lane reads its 8 consecutive k of one (ky, kx) block with two
