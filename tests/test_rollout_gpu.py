@@ -821,3 +821,84 @@ def test_rollout_mixed_n_action_mean_rows():
                 env.reset()
                 env.add_agents(h[0], method="custom", pos=left)
                 env.add_agents(h[1], method="custom", pos=right)
+
+
+def _dump_rollout(eng, E, N):
+    """Every rollout output buffer of a batch (rows < N, the rows every env wrote at its first step) and the
+    per-call getters' ids / positions / hp, as uint8 tensors on the device."""
+    import ctypes
+    import torch
+    from mfrl_amd.battle import GET_HP, GET_ID, GET_POS
+    rc, out = eng.rowcap, []
+    for name, dt in (("actions", torch.int32), ("rewards", torch.float32), ("mean_action", torch.float64),
+                     ("stats", torch.float64), ("agent_steps", torch.int64), ("group_num", torch.int32),
+                     ("episode_return", torch.float32)):
+        ptr, nb = ctypes.c_void_p(), ctypes.c_size_t()
+        eng._dll.mfx_battle_rollout_buffer(eng.game, name.encode(), 0, ctypes.byref(ptr), ctypes.byref(nb))
+        x = torch.empty(nb.value // torch.tensor([], dtype=dt).element_size(), dtype=dt, device="cuda")
+        eng.rollout_copy(name, x)
+        out.append((name, (x.view(E, 2, rc)[:, :, :N] if name in ("actions", "rewards") else x).contiguous()))
+    for g in range(2):
+        for name, w in (("view", 13 * 13 * 7), ("feature", 34)):
+            x = torch.empty(E * rc * w, dtype=torch.float32, device="cuda")
+            eng.rollout_copy(name, x, group=g)
+            out.append(("%s%d" % (name, g), x.view(E, rc, w)[:, :N].contiguous()))
+    n = torch.empty(E * 2, dtype=torch.int32, device="cuda")
+    eng.rollout_copy("group_num", n)
+    torch.cuda.synchronize()
+    for what, w, dt in ((GET_ID, 1, torch.int32), (GET_POS, 2, torch.int32), (GET_HP, 1, torch.float32)):
+        for g in range(2):
+            buf = torch.zeros((E, rc, w), dtype=dt, device="cuda")
+            eng.get(g, what, buf, rc)
+            eng.sync()
+            live = torch.arange(rc, device="cuda")[None, :] < n.view(E, 2)[:, g:g + 1]
+            out.append(("get%d_%d" % (what, g), torch.where(live[:, :, None], buf, torch.zeros_like(buf))))
+    return [(k, v.view(torch.uint8)) for k, v in out]
+
+
+def test_rollout_renumber_modes_agree(monkeypatch):
+    """The large-env slot renumbering changes where each agent's state sits, never a result: 24 staggered
+    200x200 envs (episode cap 24: restarts inside launches), 16 steps per k_rollout_bigq launch, 64 steps, with
+    the renumbering off (MFX_RENUMBER=0), on with its identity fast path (1, the default) and rewriting every
+    slot at every clear_dead (2): every output buffer and the per-call ids / positions / hp bit for bit."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, M, N, T = 24, 200, 1250, 64
+    left, right = bd.block_positions(M, N)
+    dumps = []
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("MFX_RENUMBER", mode)
+        eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=24, eps=0.3, seed=77, stagger=True)
+        eng.rollout_substeps(16)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        eng.rollout_step(T)
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, N))
+        del eng
+    for other in dumps[1:]:
+        for (k, x), (_, y) in zip(dumps[0], other):
+            assert torch.equal(x, y), k
+
+
+def test_rollout_lds_step_matches_hbm_step(monkeypatch):
+    """The few-env path's step staged in LDS (RolloutArgs::lds_step, the default) against the same step in
+    HBM (MFX_LDS_STEP=0): 64 staggered 64x64 envs, 16 steps per launch, 432 steps (every env restarts):
+    every output buffer and the per-call ids / positions / hp bit for bit."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    E, N, T = 64, 128, 432
+    left, right = bd.block_positions(64, N)
+    dumps = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MFX_LDS_STEP", mode)
+        eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1234, stagger=True)
+        eng.rollout_substeps(16)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        eng.rollout_step(T)
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, N))
+        del eng
+    for (k, x), (_, y) in zip(dumps[0], dumps[1]):
+        assert torch.equal(x, y), k
