@@ -225,8 +225,10 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
 // are staged per 16-row chunk in LDS (double buffered, the next chunk in flight in registers) and shared
 // by the four waves; LDS holds nothing else.
 constexpr int kQHeadWaves = 4, kQKC = 16;                // agents per wave = 16; weight rows per chunk
-constexpr int kQBLd = kQHObs + 16;                       // LDS stride of a staged row (16 mod 32: the 4 rows
-                                                         //   of a k-step fall on distinct banks per half-wave)
+// A staged row holds lane c's MT weights (units 16 t + c, t < MT) at c * P + t: 16-B reads of consecutive t.
+// P = MT rounded up to 4, + 4 from 8 on (a 16-lane read then spans every bank group twice at most).
+__host__ __device__ constexpr int qhead_p(int mt) { return ((mt + 3) & ~3) + (mt >= 8 ? 4 : 0); }
+constexpr int kQBLd = 16 * qhead_p(kQHObs / 16);         // the widest staged row (Dense-Obs: 320 floats)
 constexpr size_t kQHeadSmem = (size_t)2 * kQKC * kQBLd * 4;
 
 // acc[MT] = W^T . V over K (K a multiple of 4, rows of W past K read as zero).  W: [K][MT * 16] row-major.
@@ -246,11 +248,26 @@ __device__ __forceinline__ void wg_gemm_t(const float* __restrict__ W, int K, VF
             pre[j] = k < K ? W[(size_t)k * N + col] : 0.f;
         }
     };
+    constexpr int P = qhead_p(MT);
     auto store = [&](float* dst) {
 #pragma unroll
         for (int j = 0; j < MT; ++j) {
             const int q = threadIdx.x + j * 256, r = q / N, col = q - r * N;
-            dst[r * kQBLd + col] = pre[j];
+            dst[r * kQBLd + (col & 15) * P + (col >> 4)] = pre[j];
+        }
+    };
+    // this lane's MT weights of k-row kr of the staged chunk cur
+    auto read_row = [&](const float* cur, int kr, float* dst) {
+        const float* src = cur + kr * kQBLd + c * P;
+        if constexpr (MT % 4 == 0) {
+#pragma unroll
+            for (int t4 = 0; t4 < MT / 4; ++t4) {
+                const float4 x = reinterpret_cast<const float4*>(src)[t4];
+                dst[4 * t4] = x.x; dst[4 * t4 + 1] = x.y; dst[4 * t4 + 2] = x.z; dst[4 * t4 + 3] = x.w;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < MT; ++t) dst[t] = src[t];
         }
     };
 #pragma unroll
@@ -264,16 +281,11 @@ __device__ __forceinline__ void wg_gemm_t(const float* __restrict__ W, int K, VF
         // k-step s + 1's MT weights are read from LDS while k-step s's MT MFMAs issue (the compiler alone
         // waits on each read right before its MFMA)
         float av[MT], an[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) av[t] = cur[(4 * h) * kQBLd + c + t * 16];
+        read_row(cur, 4 * h, av);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const float v = v_at(ch, s);
-            if (s + 1 < 4) {
-                const float* arow = cur + (4 * h + s + 1) * kQBLd + c;
-#pragma unroll
-                for (int t = 0; t < MT; ++t) an[t] = arow[t * 16];
-            }
+            if (s + 1 < 4) read_row(cur, 4 * h + s + 1, an);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int t = 0; t < MT; ++t) acc[t] = mfma4(av[t], v, acc[t]);
