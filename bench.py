@@ -50,21 +50,22 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 49152 at 64x64, 1024 at 256x256)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 131072 at 64x64, 1024 at 256x256)")
     ap.add_argument("--total-envs", type=int, default=None,
                     help="envs over all GPUs, split evenly (strong scaling; configs[3]: --total-envs 64)")
     ap.add_argument("--map", type=int, default=MAP, help="map side (64: the metric's config; 256: configs[4])")
     ap.add_argument("--agents", type=int, default=2 * N_SIDE, help="agents per env, half per group")
     ap.add_argument("--max-steps", type=int, default=400)
-    # 4 consecutive steps of every env per k_rollout launch (env image kept in LDS between them): the
-    # launch ramp-up / tail and the env install / write-back are paid once per 4 steps, +9-11 % over one
-    # step per launch; 8 and 16 gain nothing more (profiles/r02_substeps_sweep.txt).  The results are
+    # 8 consecutive steps of every env per k_rollout launch (env image kept in LDS between them): the
+    # launch ramp-up / tail and the env install / write-back are paid once per 8 steps.  At the round-2
+    # batch of 49152 envs 4 steps gained 9-11 % over one and 8 little more (profiles/r02_substeps_sweep.txt);
+    # with 131072 envs 8 steps gain 3-4 % over 4 (profiles/r03_env_sweep.txt).  The results are
     # bit-identical for any value (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps).
     # The queue kernel k_rollout_bigq (256x256 envs, and batches of few 64x64 envs): 16 steps per launch
     # (the launch's tail is the last envs' steps): 1.19-1.20e9 against 1.15-1.18e9 at 8 and 1.0-1.07e9 at 4
     # at 256x256 (profiles/r02_bigq_sweeps.txt); 8 envs of 64x64: 0.0435 ms per step vs 0.0472 at 4.
     ap.add_argument("--substeps", type=int, default=None,
-                    help="consecutive steps of every env per launch (default 4 on k_rollout, 16 on k_rollout_bigq)")
+                    help="consecutive steps of every env per launch (default 8 on k_rollout, 16 on k_rollout_bigq)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -83,10 +84,12 @@ def parse(argv=None):
     if a.envs is None and a.total_envs is None and a.policy == "qnet":
         a.envs = 8192                 # the Q-network forward bounds this mode (3.4 MFLOP per agent-step)
     if a.envs is None and a.total_envs is None:
-        # 64x64: 49152 envs per GPU (~60 GB of observation buffers) -- a launch has a fixed cost (ramp-up
-        # and the tail of the persistent grid), amortised over more envs: at 4 steps per launch 24576 ->
-        # 32768 -> 49152 envs = 1.09 -> 1.137 -> 1.146e9 agent-steps/s (profiles/r02_env_sub_sweep.txt)
-        a.envs = 49152 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
+        # 64x64: 131072 envs per GPU (~160 GB of observation buffers, 56 % of the HBM) -- a launch has a fixed
+        # cost (ramp-up and the tail of the persistent grid: the last env of each of 1280 workgroups), amortised
+        # over more envs per workgroup: at 8 steps per launch 49152 -> 65536 -> 98304 -> 131072 envs =
+        # 1.19 -> 1.25 -> 1.30 -> 1.31-1.32e9 agent-steps/s, same box (profiles/r03_env_sweep.txt; round 2 at 4
+        # steps: 24576 -> 49152 = 1.09 -> 1.146e9, profiles/r02_env_sub_sweep.txt)
+        a.envs = 131072 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
     return a
 
 
@@ -400,7 +403,7 @@ def main():
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
     grid, lds = eng.rollout_info()          # persistent grid, LDS bytes per workgroup
-    S = max(1, args.substeps if args.substeps is not None else (16 if path == "k_rollout_bigq" else 4))
+    S = max(1, args.substeps if args.substeps is not None else (16 if path == "k_rollout_bigq" else 8))
     if S != 1:
         eng.rollout_substeps(S)
     big = path in ("k_rollout_bigq", "k_observe_items+k_rollout_big")   # large envs, state in HBM

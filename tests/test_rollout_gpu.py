@@ -322,15 +322,16 @@ def _check_launches(eng, map_size, n_side, envs, T, S, max_steps, seed, eps, pat
 
 
 def test_rollout_bench_shape_matches_oracle():
-    """The 64x64 bench exactly as bench.py runs it: 49152 staggered envs (the persistent grid is far
+    """The 64x64 bench exactly as bench.py runs it: 131072 staggered envs (the persistent grid is far
     smaller than E, so the heaviest-first class queue, the register prefetch and the queue hand-off are
-    live), 4 steps per k_rollout launch, 452 steps (every env restarts at least once; the bench's
-    preparation + warmup + timed window is 425).  16 sampled envs are replayed on the C oracle from
-    rollout_init on with the host restatement of the device rush policy, and compared after every launch.
-    Stagger: env e's first episode starts at length e * max_steps // E (BattleEngine::rollout_init)."""
+    live; view offsets past 2^31 floats), 8 steps per k_rollout launch, 456 steps (every env restarts at
+    least once; the bench's preparation + warmup + timed window is 425).  16 sampled envs are replayed on
+    the C oracle from rollout_init on with the host restatement of the device rush policy, and compared
+    after every launch.  Stagger: env e's first episode starts at length e * max_steps // E
+    (BattleEngine::rollout_init)."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, T, S, max_steps, seed = 49152, 452, 4, 400, 1234
+    E, T, S, max_steps, seed = 131072, 456, 8, 400, 1234
     left, right = bd.block_positions(64, 128)
     eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
