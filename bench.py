@@ -8,9 +8,10 @@ the warmup, so any K-step window sees the steady mix of episode phases (not just
 every env of the batch: get_observation for both groups (views + features written to HBM),
 the synthetic rush policy of SURVEY.md 8(d) (on device), set_action, step (attack shuffle,
 attacks, starve, moves, reward rules, done), get_reward, mean-action pooling, clear_dead,
-and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default 4) such
-steps of every env back to back while the env's image stays in LDS; the timed region is exactly K
-steps (K / substeps launches), bit-identical to K one-step launches.
+and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default 8) such
+steps of every env back to back while the env's image stays in LDS, for 131072 envs per GPU; the timed
+region is exactly K steps (ceil(K / substeps) launches, the last one the remainder), bit-identical to K
+one-step launches.
 `value` counts agents present at get_observation, summed over envs, steps and ranks, over the
 max-over-ranks wall time of the K timed steps.
 
