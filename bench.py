@@ -51,7 +51,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 131072 at 64x64, 1024 at 256x256)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 131072 at 64x64, 2048 at 256x256)")
     ap.add_argument("--total-envs", type=int, default=None,
                     help="envs over all GPUs, split evenly (strong scaling; configs[3]: --total-envs 64)")
     ap.add_argument("--map", type=int, default=MAP, help="map side (64: the metric's config; 256: configs[4])")
@@ -90,7 +90,10 @@ def parse(argv=None):
         # over more envs per workgroup: at 8 steps per launch 49152 -> 65536 -> 98304 -> 131072 envs =
         # 1.19 -> 1.25 -> 1.30 -> 1.31-1.32e9 agent-steps/s, same box (profiles/r03_env_sweep.txt; round 2 at 4
         # steps: 24576 -> 49152 = 1.09 -> 1.146e9, profiles/r02_env_sub_sweep.txt)
-        a.envs = 131072 if a.map * a.map <= 64 * 64 else max(8, (16384 * 256) // a.agents)
+        # 256x256 (4096 agents): 2048 envs (40 GB of observation buffers) -- 1024 -> 2048 envs at 16 steps per
+        # k_rollout_bigq launch = 1.21-1.22 -> 1.27-1.29e9 (frac 0.75 -> 0.79-0.80), 3072 loses (0.68)
+        # (profiles/r03_env_sweep256.txt)
+        a.envs = 131072 if a.map * a.map <= 64 * 64 else max(8, (32768 * 256) // a.agents)
     return a
 
 

@@ -357,12 +357,12 @@ def test_rollout_small_e_matches_oracle(E):
 
 
 def test_rollout_bigq_bench_shape_matches_oracle():
-    """The 256x256 bench (configs[4]) exactly as bench.py runs it: 1024 staggered envs of 2048 + 2048
+    """The 256x256 bench (configs[4]) exactly as bench.py runs it: 2048 staggered envs of 2048 + 2048
     agents, 16 steps per k_rollout_bigq launch, 416 steps (every env restarts, most inside a launch).
     8 sampled envs replayed on the C oracle from rollout_init on, compared after every launch."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, T, S, max_steps, seed = 1024, 416, 16, 400, 1234
+    E, T, S, max_steps, seed = 2048, 416, 16, 400, 1234
     left, right = bd.block_positions(256, 2048)
     eng = BattleBatch(256, E, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
@@ -653,7 +653,7 @@ def test_rollout_bigq_reseed_after_per_call_ops(monkeypatch):
 
 
 def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
-    """The 256x256 bench's own shape (configs[4]: 1024 staggered envs of 2048 + 2048 agents, episode cap
+    """The 256x256 bench's own shape (configs[4]: 2048 staggered envs of 2048 + 2048 agents, episode cap
     400, 16 steps per k_rollout_bigq launch) against the two-stream pipeline at one step per launch,
     after 408 steps (every env restarts at least once, inside a launch for most): every output
     buffer bit for bit (all rows the first step wrote), the episode statistics, the agent-step
@@ -661,7 +661,7 @@ def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
     import ctypes
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, M, N, T = 1024, 256, 2048, 408
+    E, M, N, T = 2048, 256, 2048, 408
     left, right = bd.block_positions(M, N)
     engs = []
     for fused, sub in (("0", 1), ("1", 16)):
