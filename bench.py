@@ -8,7 +8,7 @@ the warmup, so any K-step window sees the steady mix of episode phases (not just
 every env of the batch: get_observation for both groups (views + features written to HBM),
 the synthetic rush policy of SURVEY.md 8(d) (on device), set_action, step (attack shuffle,
 attacks, starve, moves, reward rules, done), get_reward, mean-action pooling, clear_dead,
-and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default 8) such
+and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default 20) such
 steps of every env back to back while the env's image stays in LDS, for 131072 envs per GPU; the timed
 region is exactly K steps (ceil(K / substeps) launches, the last one the remainder), bit-identical to K
 one-step launches.
@@ -57,16 +57,16 @@ def parse(argv=None):
     ap.add_argument("--map", type=int, default=MAP, help="map side (64: the metric's config; 256: configs[4])")
     ap.add_argument("--agents", type=int, default=2 * N_SIDE, help="agents per env, half per group")
     ap.add_argument("--max-steps", type=int, default=400)
-    # 8 consecutive steps of every env per k_rollout launch (env image kept in LDS between them): the
-    # launch ramp-up / tail and the env install / write-back are paid once per 8 steps.  At the round-2
+    # 20 consecutive steps of every env per launch (env image kept in LDS between them on k_rollout): the
+    # launch ramp-up / tail and the env install / write-back are paid once per 20 steps.  At the round-2
     # batch of 49152 envs 4 steps gained 9-11 % over one and 8 little more (profiles/r02_substeps_sweep.txt);
-    # with 131072 envs 8 steps gain 3-4 % over 4 (profiles/r03_env_sweep.txt).  The results are
-    # bit-identical for any value (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps).
-    # The queue kernel k_rollout_bigq (256x256 envs, and batches of few 64x64 envs): 16 steps per launch
-    # (the launch's tail is the last envs' steps): 1.19-1.20e9 against 1.15-1.18e9 at 8 and 1.0-1.07e9 at 4
-    # at 256x256 (profiles/r02_bigq_sweeps.txt); 8 envs of 64x64: 0.0435 ms per step vs 0.0472 at 4.
-    ap.add_argument("--substeps", type=int, default=None,
-                    help="consecutive steps of every env per launch (default 8 on k_rollout, 16 on k_rollout_bigq)")
+    # with 131072 envs 8 steps gain 3-4 % over 4 (profiles/r03_env_sweep.txt) and 20 another 3-4 % over 8
+    # (profiles/r03_substeps20.txt).  The queue kernel k_rollout_bigq (256x256 envs, and batches of few
+    # 64x64 envs): 20 steps per launch, +0.3 % over 16 at 60 steps, +1-2 % at 20 steps (one launch, not
+    # 16 + 4).  The results are bit-identical for any value
+    # (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps); the engine takes 1..64.
+    ap.add_argument("--substeps", type=int, default=20,
+                    help="consecutive steps of every env per launch (default 20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -407,7 +407,7 @@ def main():
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
     grid, lds = eng.rollout_info()          # persistent grid, LDS bytes per workgroup
-    S = max(1, args.substeps if args.substeps is not None else (16 if path == "k_rollout_bigq" else 8))
+    S = max(1, args.substeps)
     if S != 1:
         eng.rollout_substeps(S)
     big = path in ("k_rollout_bigq", "k_observe_items+k_rollout_big")   # large envs, state in HBM

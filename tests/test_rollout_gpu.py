@@ -324,14 +324,14 @@ def _check_launches(eng, map_size, n_side, envs, T, S, max_steps, seed, eps, pat
 def test_rollout_bench_shape_matches_oracle():
     """The 64x64 bench exactly as bench.py runs it: 131072 staggered envs (the persistent grid is far
     smaller than E, so the heaviest-first class queue, the register prefetch and the queue hand-off are
-    live; view offsets past 2^31 floats), 8 steps per k_rollout launch, 456 steps (every env restarts at
+    live; view offsets past 2^31 floats), 20 steps per k_rollout launch, 456 steps (every env restarts at
     least once; the bench's preparation + warmup + timed window is 425).  16 sampled envs are replayed on
     the C oracle from rollout_init on with the host restatement of the device rush policy, and compared
     after every launch.  Stagger: env e's first episode starts at length e * max_steps // E
     (BattleEngine::rollout_init)."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, T, S, max_steps, seed = 131072, 456, 8, 400, 1234
+    E, T, S, max_steps, seed = 131072, 456, 20, 400, 1234
     left, right = bd.block_positions(64, 128)
     eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
@@ -344,11 +344,11 @@ def test_rollout_bench_shape_matches_oracle():
 @pytest.mark.parametrize("E", [8, 64])
 def test_rollout_small_e_matches_oracle(E):
     """configs[3]'s per-GPU shape (64 envs over 8 GPUs = 8 per GPU; and 64 on one GPU) as bench.py runs it:
-    64x64 envs on the queue kernel (small_e_max), 16 steps per launch, 416 steps (every env restarts).
+    64x64 envs on the queue kernel (small_e_max), 20 steps per launch, 420 steps (every env restarts).
     Every env (E = 8) or 8 sampled envs (E = 64) replayed on the C oracle, compared after every launch."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    T, S, max_steps, seed = 416, 16, 400, 1234
+    T, S, max_steps, seed = 420, 20, 400, 1234
     left, right = bd.block_positions(64, 128)
     eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
@@ -358,11 +358,11 @@ def test_rollout_small_e_matches_oracle(E):
 
 def test_rollout_bigq_bench_shape_matches_oracle():
     """The 256x256 bench (configs[4]) exactly as bench.py runs it: 2048 staggered envs of 2048 + 2048
-    agents, 16 steps per k_rollout_bigq launch, 416 steps (every env restarts, most inside a launch).
+    agents, 20 steps per k_rollout_bigq launch, 420 steps (every env restarts, most inside a launch).
     8 sampled envs replayed on the C oracle from rollout_init on, compared after every launch."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, T, S, max_steps, seed = 2048, 416, 16, 400, 1234
+    E, T, S, max_steps, seed = 2048, 420, 20, 400, 1234
     left, right = bd.block_positions(256, 2048)
     eng = BattleBatch(256, E, stream=torch.cuda.current_stream())
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
@@ -654,17 +654,17 @@ def test_rollout_bigq_reseed_after_per_call_ops(monkeypatch):
 
 def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
     """The 256x256 bench's own shape (configs[4]: 2048 staggered envs of 2048 + 2048 agents, episode cap
-    400, 16 steps per k_rollout_bigq launch) against the two-stream pipeline at one step per launch,
-    after 408 steps (every env restarts at least once, inside a launch for most): every output
+    400, 20 steps per k_rollout_bigq launch) against the two-stream pipeline at one step per launch,
+    after 420 steps (every env restarts at least once, inside a launch for most): every output
     buffer bit for bit (all rows the first step wrote), the episode statistics, the agent-step
     counters, and no stalled queue."""
     import ctypes
     import torch
     from mfrl_amd.battle import BattleBatch
-    E, M, N, T = 2048, 256, 2048, 408
+    E, M, N, T = 2048, 256, 2048, 420
     left, right = bd.block_positions(M, N)
     engs = []
-    for fused, sub in (("0", 1), ("1", 16)):
+    for fused, sub in (("0", 1), ("1", 20)):
         monkeypatch.setenv("MFX_BIG_FUSED", fused)
         eng = BattleBatch(M, E, stream=torch.cuda.current_stream())
         eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=1234, stagger=True)
