@@ -700,7 +700,7 @@ def test_rollout_bigq_bench_shape_matches_pipeline(monkeypatch):
             del xs
 
 
-@pytest.mark.parametrize("sub", [2, 7])
+@pytest.mark.parametrize("sub", [2, 7, 20, 64])
 def test_rollout_substeps_match_single_steps(sub):
     """k_rollout running `sub` consecutive steps of each env per launch (image kept in LDS) leaves
     exactly what single-step launches leave: every output buffer, the episode statistics, the
