@@ -97,6 +97,19 @@ def parse(argv=None):
     return a
 
 
+def rank_device(world, local, device_count, backend):
+    """(device index of this rank, GPUs the job spans).  RCCL ("nccl") needs one GPU per rank: a world larger
+    than the node's device count is refused, not wrapped onto shared cards.  Other backends (gloo rehearsals
+    of the N-rank flow on one card) wrap local ranks over the devices, and the line reports the GPUs they
+    actually span beside the rank count."""
+    if device_count < 1:
+        raise RuntimeError("bench.py: no GPU visible")
+    if backend == "nccl" and world > device_count:
+        raise RuntimeError("bench.py: %d ranks over RCCL need %d GPUs, this node shows %d (ranks never share a GPU "
+                           "under RCCL; rehearse with --backend gloo)" % (world, world, device_count))
+    return local % device_count, min(world, device_count)
+
+
 def rank_envs(args, world, rank):
     """Envs this rank steps: --envs per rank, or its share of --total-envs (remainder to low ranks)."""
     if args.total_envs is None:
@@ -391,8 +404,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())     # (rehearsals: several ranks on one GPU)
+    local, n_gpus = rank_device(world, int(os.environ.get("LOCAL_RANK", "0")), torch.cuda.device_count(),
+                                args.backend if world > 1 else "nccl")
     torch.cuda.set_device(local)
     if world > 1:
         if args.backend == "nccl":           # RCCL over xGMI
@@ -479,7 +492,7 @@ def main():
             "metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents" % (args.map, args.map, args.agents),
             "value": total_units / elapsed,
             "unit": "agent-steps/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": n_gpus, "ranks": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
@@ -496,7 +509,8 @@ def main():
                        # agents placed per episode start vs the live agents an env-step actually carries (the
                        # unit counts live agents; battles thin the armies, staggered episodes mix all phases)
                        "live_agents_per_env_step": local_units / (args.steps * E),
-                       "parallelism": "envs sharded one process per GPU (dp%d)" % world},
+                       "parallelism": ("envs sharded one process per GPU (dp%d)" % world) if n_gpus == world else
+                                      ("%d ranks on %d GPU(s), %s rehearsal" % (world, n_gpus, args.backend))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kernel_ms,
@@ -506,7 +520,11 @@ def main():
                          "grid": grid, "lds_bytes": lds},
             "cpu_baseline": None,
             "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],
-                         "kills": red[3], "note": "all ranks, since rollout_init (RCCL all-reduce per episode batch)"},
+                         "kills": red[3],
+                         "note": "all ranks, since rollout_init (%s)" % (
+                             "one rank: reduced locally after the clock" if world == 1 else
+                             "RCCL all-reduce over xGMI per episode batch" if args.backend == "nccl" else
+                             "%s all-reduce per episode batch: a rehearsal of the N-rank flow, not RCCL" % args.backend)},
         }
         if check is not None:
             line["check"] = check

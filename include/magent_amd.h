@@ -121,6 +121,8 @@ int mfx_battle_rollout_copy(void *game, const char *name, int group, void *dst, 
 /* bytes [offset, offset + bytes) of a rollout buffer (e.g. one env's rows), async on the engine stream */
 int mfx_battle_rollout_copy_at(void *game, const char *name, int group, size_t offset, void *dst, size_t bytes);
 int mfx_battle_rollout_rowcap(void *game, int *rowcap);
+/* Doubles per [env][group] row of the rollout's mean-action buffer (the largest n_action of the groups). */
+int mfx_battle_rollout_mean_stride(void *game, int *stride);
 /* Persistent grid (workgroups per launch) and dynamic LDS bytes per workgroup of the fused rollout. */
 int mfx_battle_rollout_info(void *game, int *grid, int *lds_bytes);
 /* Synchronises the engine stream; -1 (message in mfx_last_error) if a device error was raised or, on the
@@ -187,9 +189,12 @@ int mfx_qnet_act_rollout(void *handle, const float *d_view, const float *d_feat,
 /* ---------------------------------------------------------------- part 6: replay rows */
 /* The data path of the replay buffers (algo/tools.py:26-362): for i < n, row idx[i] (or i; modulo src_mod
  * when > 0) of every source column -> row dst_start + i (modulo dst_cap when > 0) of its destination column;
- * n_cols <= 8, row_bytes per column; one launch (csrc/replay_kernels.hip). */
+ * n_cols <= 8, row_bytes per column; one launch (csrc/replay_kernels.hip).  src_rows: rows of every source
+ * column -- a source index outside it (the reference's numpy indexing raises IndexError) skips the row and is
+ * reported by mfx_rows_copy_error (synchronising; -1 and *bad_index when one was met, then cleared). */
 int mfx_rows_copy(int n_cols, void *const *dst, const void *const *src, const int64_t *row_bytes, const int64_t *d_idx,
-                  int64_t src_mod, int64_t dst_start, int64_t dst_cap, int64_t n, void *stream);
+                  int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap, int64_t n, void *stream);
+int mfx_rows_copy_error(int64_t *bad_index, void *stream);
 
 /* ---------------------------------------------------------------- library */
 const char *mfx_last_error(void);

@@ -860,8 +860,8 @@ public:
             MFX_HIP(hipMemsetAsync(d_err, 0, sizeof(int32_t), stream));
             static const char* msg[] = {"", "", "agent capacity exceeded", "no blank position for random placement",
                                         "output row capacity smaller than the group", "invalid action id",
-                                        "action buffer overflow"};
-            return fail("device error %d: %s", h, h > 0 && h < 7 ? msg[h] : "unknown");
+                                        "action buffer overflow", "move claim table outside the step scratch"};
+            return fail("device error %d: %s", h, h > 0 && h < 8 ? msg[h] : "unknown");
         }
         return 0;
     }
@@ -874,8 +874,8 @@ public:
         MFX_HIP(hipMemsetAsync(d_err, 0, sizeof(int32_t), stream));
         static const char* msg[] = {"", "", "agent capacity exceeded", "no blank position for random placement",
                                     "output row capacity smaller than the group", "invalid action id",
-                                    "action buffer overflow"};
-        return fail("device error %d: %s", h, h > 0 && h < 7 ? msg[h] : "unknown");
+                                    "action buffer overflow", "move claim table outside the step scratch"};
+        return fail("device error %d: %s", h, h > 0 && h < 8 ? msg[h] : "unknown");
     }
 
     // env 0's record (k_get_env0): 64-B header (group sizes, error word, done), then per group
@@ -2357,6 +2357,10 @@ MFX_API int mfx_battle_rollout_set_substeps(void* game, int n_sub) {
 
 MFX_API int mfx_battle_rollout_rowcap(void* game, int* rowcap) {
     *rowcap = MFX_ENV(game)->ra.rowcap;
+    return 0;
+}
+MFX_API int mfx_battle_rollout_mean_stride(void* game, int* stride) {
+    *stride = MFX_ENV(game)->ra.mean_stride;
     return 0;
 }
 MFX_API int mfx_battle_group_capacity(void* game, int group, int* cap) {

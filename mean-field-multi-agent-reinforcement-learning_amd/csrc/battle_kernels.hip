@@ -29,6 +29,7 @@ constexpr int kStampW = 32;                  // stamps per env row
         if (TID == 0 && g_stamps) {                                                         \
             g_stamps[stamp_row * kStampW + (i)] = __builtin_amdgcn_s_memtime();                  \
             if ((i) == 0) g_stamps[stamp_row * kStampW + 11] = __builtin_amdgcn_s_memrealtime();  \
+            if ((i) == 0) g_stamps[stamp_row * kStampW + 28] = blockIdx.x;                        \
             if ((i) == 10) g_stamps[stamp_row * kStampW + 12] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                                   \
     } while (0)

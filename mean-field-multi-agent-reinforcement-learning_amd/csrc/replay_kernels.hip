@@ -66,16 +66,25 @@ __device__ __forceinline__ void row_copy16(const uint4* __restrict__ sp, uint4* 
     }
 }
 
+// First out-of-range source index seen by k_rows_copy, plus one (0: none); read and cleared by
+// mfx_rows_copy_error.  A bad row is skipped, never read.
+__device__ unsigned long long g_rows_bad;
+
 // One wave per row (four rows per workgroup): row s = idx ? idx[i] : i (modulo src_mod) of every column to
 // row d = dst_start + i (modulo dst_cap).  The narrow columns in one pass of unit loads, then each wide
 // column with its loads issued ahead of its stores -- a row is ~5 KB, so a wave keeps 2 KB in flight.
+// Source rows outside [0, src_rows) are skipped and reported (g_rows_bad).
 __global__ void __launch_bounds__(256) k_rows_copy(RowCols c, const int64_t* __restrict__ idx, int64_t src_mod,
-                                                   int64_t dst_start, int64_t dst_cap, int64_t n) {
+                                                   int64_t src_rows, int64_t dst_start, int64_t dst_cap, int64_t n) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * 4;
     for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += waves) {
         int64_t s = idx ? idx[i] : i;
         if (src_mod > 0) { s %= src_mod; if (s < 0) s += src_mod; }
+        if (s < 0 || s >= src_rows) {
+            if (lane == 0) atomicCAS(&g_rows_bad, 0ull, (unsigned long long)(idx ? idx[i] : i) + 1ull);
+            continue;
+        }
         int64_t d = dst_start + i;
         if (dst_cap > 0 && d >= dst_cap) d %= dst_cap;
         for (int u = lane; u < c.ustart[kRowCols]; u += 64) {
@@ -115,10 +124,16 @@ extern "C" {
 // to row d = dst_start + i (modulo dst_cap when dst_cap > 0) of the destination column.  n_cols <= 8;
 // row_bytes[k]: bytes per row of column k.  Destination rows of one call must be distinct (a ring shorter
 // than n would make two rows race for a slot: the caller skips the rows a ring would overwrite).
+// src_rows: rows every source column holds; an index outside [0, src_rows) (after the modulo) skips its row and
+// is reported by mfx_rows_copy_error.
 MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, const int64_t* row_bytes,
-                          const int64_t* d_idx, int64_t src_mod, int64_t dst_start, int64_t dst_cap, int64_t n,
-                          void* stream) {
+                          const int64_t* d_idx, int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap,
+                          int64_t n, void* stream) {
     if (n_cols < 1 || n_cols > kRowCols) return fail("rows_copy: 1..%d columns, got %d", kRowCols, n_cols);
+    if (src_mod > src_rows) return fail("rows_copy: modulo %lld over %lld source rows", (long long)src_mod,
+                                        (long long)src_rows);
+    if (!d_idx && n > src_rows) return fail("rows_copy: %lld rows from %lld source rows", (long long)n,
+                                            (long long)src_rows);
     if (n < 0 || (dst_cap > 0 && n > dst_cap)) return fail("rows_copy: %lld rows into a ring of %lld", (long long)n,
                                                            (long long)dst_cap);
     if (n == 0) return 0;
@@ -142,9 +157,22 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
     for (int k = n_cols; k <= kRowCols; ++k) c.ustart[k] = units;
     const int64_t wgs = (n + 3) / 4;
     const int grid = (int)(wgs < 65536 ? wgs : 65536);
-    k_rows_copy<<<grid, 256, 0, (hipStream_t)stream>>>(c, d_idx, src_mod, dst_start, dst_cap, n);
+    k_rows_copy<<<grid, 256, 0, (hipStream_t)stream>>>(c, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
     MFX_HIP(hipGetLastError());
     return 0;
+}
+
+// Synchronises `stream`; *bad_index = the first out-of-range source index any k_rows_copy met since the last
+// call (-1: none), and the word is cleared.  Returns -1 (with the message) when one was met.
+MFX_API int mfx_rows_copy_error(int64_t* bad_index, void* stream) {
+    unsigned long long h = 0;
+    MFX_HIP(hipStreamSynchronize((hipStream_t)stream));
+    MFX_HIP(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_rows_bad), sizeof(h), 0, hipMemcpyDeviceToHost));
+    *bad_index = h ? (int64_t)(h - 1ull) : -1;
+    if (!h) return 0;
+    const unsigned long long z = 0;
+    MFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rows_bad), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+    return fail("rows_copy: source index %lld out of range (row skipped)", (long long)*bad_index);
 }
 
 }  // extern "C"

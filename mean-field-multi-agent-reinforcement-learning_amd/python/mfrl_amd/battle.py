@@ -33,7 +33,7 @@ class BattleBatch:
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
                    "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check", "mfx_battle_rollout_path",
-                   "mfx_battle_rollout_policy_step", "mfx_battle_rollout_sum_lanes"):
+                   "mfx_battle_rollout_policy_step", "mfx_battle_rollout_sum_lanes", "mfx_battle_rollout_mean_stride"):
             try:
                 getattr(self._dll, fn).restype = ctypes.c_int
             except AttributeError:          # an older build of the library (A/B runs)
@@ -160,11 +160,11 @@ class BattleBatch:
         self._check(self._dll.mfx_battle_rollout_policy_step(self.game, 1), "rollout_policy_step")
 
     def mean_stride(self):
-        """Doubles per [env][group] row of the mean-action buffer (the largest n_action)."""
-        p, nb = ctypes.c_void_p(), ctypes.c_size_t()
-        self._check(self._dll.mfx_battle_rollout_buffer(self.game, b"mean_action", 0, ctypes.byref(p),
-                                                        ctypes.byref(nb)), "rollout_buffer")
-        return nb.value // 8 // (self.n_envs * len(self.handles))
+        """Doubles per [env][group] row of the mean-action buffer (the largest n_action), as the engine laid
+        it out (the buffer itself may be larger: device buffers are kept across re-initialisations)."""
+        p = ctypes.c_int()
+        self._check(self._dll.mfx_battle_rollout_mean_stride(self.game, ctypes.byref(p)), "rollout_mean_stride")
+        return p.value
 
     def rollout_copy(self, name, dst, group=0, nbytes=None):
         """Copy a device rollout buffer into dst (numpy array or torch tensor, host or device)."""

@@ -14,7 +14,9 @@ _MAX_COLS = 8
 def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
     """For i < n: row (idx[i] if idx is not None else i), taken modulo src_mod if > 0, of every tensor in
     `src` -> row dst_start + i (modulo dst_cap if > 0) of the matching tensor in `dst`.  Tensors: CUDA,
-    contiguous, first dimension = rows, equal row byte sizes pairwise."""
+    contiguous, first dimension = rows, equal row byte sizes pairwise.  A source index outside the source
+    rows is skipped on the device and raised by the next check() (the reference's numpy indexing raises
+    IndexError at once; checking here would synchronise every move)."""
     assert len(dst) == len(src) and 0 < len(dst) <= _MAX_COLS
     if n is None:
         n = len(idx) if idx is not None else src[0].shape[0]
@@ -29,11 +31,23 @@ def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
     if idx is not None:
         idx = idx.to(device=dst[0].device, dtype=torch.int64).contiguous()
     k = len(dst)
+    src_rows = min(s.shape[0] for s in src)
     L = lib()
     L.mfx_rows_copy.restype = ctypes.c_int
     P = ctypes.c_void_p * k
     check(L.mfx_rows_copy(k, P(*[d.data_ptr() for d in dst]), P(*[s.data_ptr() for s in src]),
                           (ctypes.c_int64 * k)(*rb), ctypes.c_void_p(idx.data_ptr() if idx is not None else 0),
-                          ctypes.c_int64(int(src_mod)), ctypes.c_int64(int(dst_start)), ctypes.c_int64(int(dst_cap)),
-                          ctypes.c_int64(int(n)), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                          ctypes.c_int64(int(src_mod)), ctypes.c_int64(int(src_rows)), ctypes.c_int64(int(dst_start)),
+                          ctypes.c_int64(int(dst_cap)), ctypes.c_int64(int(n)),
+                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
           "mfx_rows_copy")
+
+
+def check():
+    """Synchronise the current stream; raise IndexError if a rows_copy since the last check met a source
+    index outside its source rows (that row was skipped)."""
+    L = lib()
+    L.mfx_rows_copy_error.restype = ctypes.c_int
+    bad = ctypes.c_int64()
+    if L.mfx_rows_copy_error(ctypes.byref(bad), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
+        raise IndexError("rows_copy: source index %d out of range" % bad.value)

@@ -11,6 +11,10 @@ against the reference's own senario_battle.generate_map.  OMP_NUM_THREADS must b
 the reference attack loop is racy with more threads.
 
 Output: tests/golden/battle_*.npz (numeric arrays only, no pickles) + manifest.json.
+
+    OMP_NUM_THREADS=1 python tests/golden/make_battle_fixtures.py battle256_seq battle256_rollout
+
+regenerates only the named cases (the manifest's other entries are kept).
 """
 import ctypes
 import importlib.util
@@ -101,16 +105,41 @@ def pack_episode(rec, prefix, out, keep_raw):
     return T
 
 
-def main():
+def main(only=()):
     gw, battle_cfg, scen = load_reference_magent()
     manifest = {"generator": "tests/golden/make_battle_fixtures.py",
                 "engine": "reference MAgent (oracle/_ref, OMP_NUM_THREADS=1) via reference gridworld.py",
                 "cases": {}}
+    if only:
+        with open(os.path.join(HERE, "battle_manifest.json")) as f:
+            manifest = json.load(f)
+
+    def want(name):
+        return not only or name in only
 
     def new_env(map_size):
         env = gw.GridWorld(battle_cfg.get_config(map_size))
         return env, env.get_handles()
 
+    if want("battle40"):
+        case_battle40(new_env, scen, manifest)
+    if want("battle64"):
+        case_battle64(new_env, manifest)
+    if want("battle256"):
+        case_battle256(new_env, manifest)
+    if want("battle_edge16"):
+        case_edge16(new_env, manifest)
+    if want("battle256_seq"):
+        case_battle256_seq(new_env, manifest)
+    if want("battle256_rollout"):
+        case_battle256_rollout(new_env, manifest)
+
+    with open(os.path.join(HERE, "battle_manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print(json.dumps(manifest, indent=1))
+
+
+def case_battle40(new_env, scen, manifest):
     # 1) 40x40 generate_map, three seeds; seed 0 runs two episodes in ONE env (LCG persistence)
     out = {}
     env, handles = new_env(40)
@@ -143,6 +172,9 @@ def main():
         manifest["cases"]["battle40_s%d" % seed] = {"map_size": 40, "episodes": [
             {"seed": seed, "policy_seed": seed, "steps": T, "placement": "generate_map"}]}
 
+
+
+def case_battle64(new_env, manifest):
     # 2) 64x64, 128 per side (8x16 blocks) -- the headline config
     out = {}
     env, handles = new_env(64)
@@ -154,6 +186,9 @@ def main():
     manifest["cases"]["battle64"] = {"map_size": 64, "episodes": [
         {"seed": None, "policy_seed": 7, "steps": T, "placement": "blocks128"}]}
 
+
+
+def case_battle256(new_env, manifest):
     # 3) 256x256, 2048 per side -- large-map band mode; hashes only, 60 steps
     out = {}
     env, handles = new_env(256)
@@ -165,10 +200,14 @@ def main():
     manifest["cases"]["battle256"] = {"map_size": 256, "episodes": [
         {"seed": None, "policy_seed": 11, "steps": T, "placement": "blocks2048"}]}
 
+
+
+def case_edge16(new_env, manifest):
     # 4) edge: 16x16, 1 vs 6 agents, walls; one side is wiped out -> after clear_dead the
     #    survivors' minimap channel of the empty group is 0/0 (NaN in the reference).
     out = {}
     env, handles = new_env(16)
+    _, v2a = env.get_view2attack(handles[0])
     env.reset()
     env.add_walls(method="custom", pos=[(5, 5), (5, 6), (5, 7), (9, 3)])
     env.add_agents(handles[0], method="custom", pos=[(7, 7, 0)])
@@ -207,10 +246,93 @@ def main():
                                           "note": "custom walls, duplicate placement skipped, "
                                                   "group wiped -> NaN minimap after clear_dead"}
 
-    with open(os.path.join(HERE, "battle_manifest.json"), "w") as f:
-        json.dump(manifest, f, indent=1)
-    print(json.dumps(manifest, indent=1))
+
+def case_battle256_seq(new_env, manifest):
+    # 5) 256x256, 2048 per side, TWO full episodes (<= 400 steps each) in ONE env under the rush
+    #    policy: the large-map band order late in a fight (thinned map, clear_dead churn) and the
+    #    attack-shuffle LCG carried across an episode restart in band mode (GridWorld.cc:79-89,
+    #    :437-478, :662-672).  Hashes + actions only.
+    out = {}
+    env, handles = new_env(256)
+    placement = bd.placement_blocks(256, 2048)
+    episodes = []
+    for ep, pseed in enumerate((21, 22)):
+        rec = bd.run_episode(env, handles, placement, 400, policy_seed=pseed, keep_raw=False)
+        T = pack_episode(rec, "e%d_" % ep, out, False)
+        episodes.append({"seed": None, "policy_seed": pseed, "steps": T, "placement": "blocks2048"})
+    del env
+    np.savez_compressed(os.path.join(HERE, "battle256_seq.npz"), **out)
+    manifest["cases"]["battle256_seq"] = {"map_size": 256, "episodes": episodes,
+                                          "note": "two full episodes in one env (band mode, LCG persistence)"}
+
+
+def case_battle256_rollout(new_env, manifest, E=2048, seed=1234, eps=0.2, max_steps=400, episodes=2):
+    # 6) env 0 of the 256x256 bench batch (bench.py: E staggered envs, env 0 starts at episode length 0)
+    #    under the DEVICE rush policy (tests/rollout_check.py device_rush_actions: a counter hash of
+    #    seed / env / step / id), recorded on the reference engine through the reference wrapper: a
+    #    k_rollout_bigq launch of that batch must reproduce it at every launch boundary.
+    import rollout_check as rck
+    env, h = new_env(256)
+    placement = bd.placement_blocks(256, 2048)
+    G = len(h)
+    n_action = int(env.get_action_space(h[0])[0])
+    attack_base, v2a = env.get_view2attack(h[0])
+    rec = {k: [] for k in ("n", "sha_view", "sha_feat", "sha_ids", "sha_reward", "sha_alive", "sha_pos",
+                           "sha_ids_cd", "sha_pos_cd", "num_after", "done", "rsum512", "ep_len")}
+    acts_all = []
+
+    def reset():
+        env.reset()
+        for g, pos in placement:
+            env.add_agents(h[g], method="custom", pos=pos)
+
+    reset()
+    t, ep, ep_len = 0, 0, 0
+    while ep < episodes:
+        obs = [tuple(x.copy() for x in env.get_observation(h[g])) for g in range(G)]
+        ids = [env.get_agent_id(h[g]) for g in range(G)]
+        acts = [rck.device_rush_actions(obs[g][0], obs[g][1], ids[g], g, 0, t, seed, eps, v2a, attack_base, n_action)
+                for g in range(G)]
+        for g in range(G):
+            env.set_action(h[g], acts[g])
+        done = env.step()
+        rew = [env.get_reward(h[g]) for g in range(G)]
+        rec["n"].append([len(x) for x in ids])
+        rec["sha_view"].append([bd.sha(o[0]) for o in obs])
+        rec["sha_feat"].append([bd.sha(o[1]) for o in obs])
+        rec["sha_ids"].append([bd.sha(x) for x in ids])
+        rec["sha_reward"].append([bd.sha(r) for r in rew])
+        rec["sha_alive"].append([bd.sha(env.get_alive(h[g])) for g in range(G)])
+        rec["sha_pos"].append([bd.sha(env.get_pos(h[g])) for g in range(G)])
+        rec["rsum512"].append([rck.device_sum(r, 512) for r in rew])
+        rec["done"].append(bool(done))
+        acts_all.append(acts)
+        env.clear_dead()
+        rec["sha_ids_cd"].append([bd.sha(env.get_agent_id(h[g])) for g in range(G)])
+        rec["sha_pos_cd"].append([bd.sha(env.get_pos(h[g])) for g in range(G)])
+        rec["num_after"].append([env.get_num(h[g]) for g in range(G)])
+        ep_len += 1
+        rec["ep_len"].append(ep_len)
+        if done or ep_len >= max_steps:
+            ep += 1
+            ep_len = 0
+            reset()
+        t += 1
+    out = {"n": np.array(rec["n"], dtype=np.int32), "num_after": np.array(rec["num_after"], dtype=np.int32),
+           "done": np.array(rec["done"], dtype=np.bool_), "rsum512": np.array(rec["rsum512"], dtype=np.float32),
+           "ep_len": np.array(rec["ep_len"], dtype=np.int32),
+           "actions": np.concatenate([a for row in acts_all for a in row]).astype(np.int8)}
+    for k in ("sha_view", "sha_feat", "sha_ids", "sha_reward", "sha_alive", "sha_pos", "sha_ids_cd", "sha_pos_cd"):
+        out[k] = np.frombuffer(b"".join(b for row in rec[k] for b in row), dtype=np.uint8).reshape(t, G, 32)
+    del env
+    np.savez_compressed(os.path.join(HERE, "battle256_rollout.npz"), **out)
+    manifest["cases"]["battle256_rollout"] = {
+        "map_size": 256, "placement": "blocks2048", "steps": t, "env": 0, "n_envs": E, "seed": seed, "eps": eps,
+        "max_steps": max_steps, "episodes": episodes,
+        "note": "env 0 of the staggered bench batch under the device rush policy; per step: obs / ids / "
+                "rewards / alive / pos hashes, post-clear_dead ids / pos hashes, actions, reward sums in the "
+                "512-lane device order"}
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

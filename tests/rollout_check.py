@@ -109,6 +109,8 @@ class EnvReplay:
 
     def __init__(self, map_size, placement, env, E, max_steps, stagger, seed, eps, path, lib=None, lanes=None):
         self.oracle, self.h = common.battle_env(lib or common.ORACLE_LIB, map_size)
+        # the reference build has no "hp" info (its hp shows only in the views): state() skips it there
+        self.has_hp = lib is None or lib == common.ORACLE_LIB
         self.placement = placement
         self.e, self.seed, self.eps, self.path, self.max_steps = env, seed, eps, path, max_steps
         self.lanes = lanes
@@ -169,7 +171,8 @@ class EnvReplay:
         o, h = self.oracle, self.h
         return {"ids": [o.get_agent_id(h[g]) for g in range(self.G)],
                 "pos": [o.get_pos(h[g]) for g in range(self.G)],
-                "hp": [o._info_array(h[g], b"hp", (o.get_num(h[g]),), np.float32) for g in range(self.G)]}
+                "hp": [o._info_array(h[g], b"hp", (o.get_num(h[g]),), np.float32) if self.has_hp else None
+                       for g in range(self.G)]}
 
 
 def device_records(eng, envs):
@@ -251,7 +254,7 @@ def compare(dev, j, rep, tag=""):
             bad.append("%s group %d: ids" % (tag, g))
         if dev["pos"][g][j, :m].tobytes() != st["pos"][g].tobytes():
             bad.append("%s group %d: positions" % (tag, g))
-        if dev["hp"][g][j, :m, 0].tobytes() != st["hp"][g].tobytes():
+        if st["hp"][g] is not None and dev["hp"][g][j, :m, 0].tobytes() != st["hp"][g].tobytes():
             bad.append("%s group %d: hp" % (tag, g))
     return bad
 
@@ -284,3 +287,101 @@ class RolloutChecker:
             rep.advance(T)
             bad += compare(dev, j, rep, "env %d step %d:" % (self.envs[j], T))
         return bad
+
+
+# --------------------------------------------------------------------------------------------------------
+# the reference-recorded rollout fixture (tests/golden/battle256_rollout.npz, make_battle_fixtures.py):
+# env 0 of the 256x256 bench batch under the device rush policy, recorded on the reference engine itself
+# --------------------------------------------------------------------------------------------------------
+class RolloutFixture:
+    """Expected per-launch-boundary records of env `case["env"]` from the reference recording."""
+
+    def __init__(self, name="battle256_rollout"):
+        self.case = common.manifest()["cases"][name]
+        self.fx = np.load(common.GOLDEN + "/" + name + ".npz")
+        self.n = self.fx["n"]
+        self.acts = common.unpack_actions(self.fx, "", self.n)
+        self.placement = bd.block_positions(self.case["map_size"], int(self.case["placement"].replace("blocks", "")))
+        T = len(self.n)
+        # running quantities of the device's counters, step by step
+        self.agent_steps = np.cumsum(self.n.sum(1)).astype(np.int64)
+        self.stats = np.zeros((T, 4), dtype=np.float64)
+        self.ep_return = np.zeros((T, self.n.shape[1]), dtype=np.float32)
+        st, ret = np.zeros(4, dtype=np.float64), np.zeros(self.n.shape[1], dtype=np.float32)
+        self.restart = np.zeros(T, dtype=bool)
+        for t in range(T):
+            ret = (ret + self.fx["rsum512"][t]).astype(np.float32)
+            st[3] += float((self.n[t] - self.fx["num_after"][t]).sum())
+            if self.fx["done"][t] or self.fx["ep_len"][t] >= self.case["max_steps"]:
+                self.restart[t] = True
+                st[0] += 1.0
+                st[1] += float(ret[0])
+                st[2] += float(ret[1])
+                ret[:] = 0.0
+            self.stats[t], self.ep_return[t] = st, ret
+
+    def compare(self, dev, j, t):
+        """Mismatches between slot j of device_records (taken after global step t) and the recording."""
+        fx, bad, tag = self.fx, [], "step %d:" % t
+        if int(dev["agent_steps"][j]) != int(self.agent_steps[t]):
+            bad.append("%s agent_steps %d != %d" % (tag, int(dev["agent_steps"][j]), int(self.agent_steps[t])))
+        if dev["stats"][j].tobytes() != self.stats[t].tobytes():
+            bad.append("%s stats %s != %s" % (tag, dev["stats"][j].tolist(), self.stats[t].tolist()))
+        if dev["ep_return"][j].tobytes() != self.ep_return[t].tobytes():
+            bad.append("%s episode return %s != %s" % (tag, dev["ep_return"][j].tolist(), self.ep_return[t].tolist()))
+        for g in range(self.n.shape[1]):
+            n = int(self.n[t, g])
+            if bd.sha(dev["view"][g][j, :n]) != fx["sha_view"][t, g].tobytes():
+                bad.append("%s group %d: view" % (tag, g))
+            if bd.sha(dev["feature"][g][j, :n]) != fx["sha_feat"][t, g].tobytes():
+                bad.append("%s group %d: feature" % (tag, g))
+            a = self.acts[t][g]
+            if dev["actions"][j, g, :n].tobytes() != a.astype(np.int32).tobytes():
+                bad.append("%s group %d: actions" % (tag, g))
+            if bd.sha(dev["rewards"][j, g, :n]) != fx["sha_reward"][t, g].tobytes():
+                bad.append("%s group %d: rewards" % (tag, g))
+            NA = dev["mean"].shape[2]
+            mean = np.bincount(a, minlength=NA) / n if n else np.full(NA, np.nan)
+            if not np.array_equal(dev["mean"][j, g, :NA], mean, equal_nan=True):
+                bad.append("%s group %d: mean action" % (tag, g))
+            m = int(dev["group_num"][j, g])
+            if self.restart[t]:               # the env restarted inside the launch: the reset placement
+                base = sum(len(p) for p in self.placement[:g])
+                want_m = len(self.placement[g])
+                ids_ok = m == want_m and np.array_equal(dev["ids"][g][j, :m, 0], np.arange(base, base + m))
+                pos_ok = m == want_m and np.array_equal(dev["pos"][g][j, :m], np.asarray(self.placement[g])[:, :2])
+            else:
+                want_m = int(fx["num_after"][t, g])
+                ids_ok = m == want_m and bd.sha(dev["ids"][g][j, :m, 0]) == fx["sha_ids_cd"][t, g].tobytes()
+                pos_ok = m == want_m and bd.sha(dev["pos"][g][j, :m]) == fx["sha_pos_cd"][t, g].tobytes()
+            if m != want_m:
+                bad.append("%s group %d: size %d != %d" % (tag, g, m, want_m))
+            elif not ids_ok:
+                bad.append("%s group %d: ids" % (tag, g))
+            elif not pos_ok:
+                bad.append("%s group %d: positions" % (tag, g))
+        return bad
+
+
+def replay_records(rep):
+    """An EnvReplay's last step and state in the layout of device_records (one slot), so that
+    RolloutFixture.compare can check the oracle replay itself against the reference recording."""
+    last, st, G = rep.last, rep.state(), rep.G
+    rc = max([1] + last["n"] + [len(x) for x in st["ids"]])
+    NA = len(last["mean"][0])
+    out = {"agent_steps": np.array([rep.agent_steps]), "stats": rep.stats[None].copy(),
+           "ep_return": rep.ep_return[None].copy(), "view": [], "feature": [],
+           "actions": np.zeros((1, G, rc), np.int32), "rewards": np.zeros((1, G, rc), np.float32),
+           "mean": np.zeros((1, G, NA), np.float64), "group_num": np.zeros((1, G), np.int32),
+           "ids": [], "pos": []}
+    for g in range(G):
+        n, m = last["n"][g], len(st["ids"][g])
+        out["view"].append(last["view"][g].reshape(1, n, -1))
+        out["feature"].append(last["feature"][g].reshape(1, n, -1))
+        out["actions"][0, g, :n] = last["actions"][g]
+        out["rewards"][0, g, :n] = last["rewards"][g]
+        out["mean"][0, g] = last["mean"][g]
+        out["group_num"][0, g] = m
+        out["ids"].append(np.asarray(st["ids"][g], np.int32).reshape(1, m, 1))
+        out["pos"].append(np.asarray(st["pos"][g], np.int32).reshape(1, m, 2))
+    return out

@@ -26,8 +26,12 @@ def test_hip_replays_reference_fixture(name, fast, monkeypatch):
     assert common.replay_case(common.HIP_LIB, name) == []
 
 
-def test_hip_replays_reference_large_map():
-    assert common.replay_case(common.HIP_LIB, "battle256") == []
+@pytest.mark.parametrize("name", ["battle256", "battle256_seq"])
+def test_hip_replays_reference_large_map(name):
+    """256x256 / 4096 agents through the per-call ABI (k_step_big: band-sorted moves, attack_big):
+    the 60-step opening, and two full 400-step episodes in one env (late-game band order on the
+    thinned map, the LCG carried across the restart)."""
+    assert common.replay_case(common.HIP_LIB, name) == []
 
 
 def test_hip_full_observation_tensors():

@@ -94,3 +94,17 @@ def test_cpu_baseline_uses_several_cores():
     assert res["value"] > 0 and abs(res["per_core"] * 2 - res["value"]) < 1e-6
     use, shown = bench.host_cores()
     assert 1 <= use <= shown
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus():
+    """Under RCCL every rank needs its own GPU: a world above the device count fails loudly instead of
+    wrapping ranks onto shared cards; gloo rehearsals wrap and report the GPUs actually spanned."""
+    import bench
+    assert bench.rank_device(8, 5, 8, "nccl") == (5, 8)
+    assert bench.rank_device(1, 0, 1, "nccl") == (0, 1)
+    with pytest.raises(RuntimeError, match="need 2 GPUs"):
+        bench.rank_device(2, 1, 1, "nccl")
+    assert bench.rank_device(2, 1, 1, "gloo") == (0, 1)
+    assert bench.rank_device(3, 2, 2, "gloo") == (0, 2)
+    with pytest.raises(RuntimeError):
+        bench.rank_device(1, 0, 0, "nccl")

@@ -43,3 +43,24 @@ def test_oracle_full_observation_tensors():
 def test_oracle_edge_case_nan_minimap():
     import edge_case
     edge_case.check(common.ORACLE_LIB)
+
+
+@pytest.mark.parametrize("name", ["battle256_seq"])
+def test_oracle_replays_reference_full_large_episodes(name):
+    """256x256, 2048 per side: two full 400-step episodes in one env (band-mode move order on the
+    thinned late-game map, clear_dead churn, the attack-shuffle LCG carried across the restart)."""
+    assert common.replay_case(common.ORACLE_LIB, name) == []
+
+
+def test_oracle_replays_reference_rollout_fixture():
+    """Env 0 of the 256x256 bench batch under the device rush policy (restated on the host), two
+    episodes, on the C oracle: every step equals the reference recording (tests/golden/battle256_rollout)."""
+    import rollout_check as rck
+    fx = rck.RolloutFixture()
+    c = fx.case
+    rep = rck.EnvReplay(c["map_size"], fx.placement, c["env"], c["n_envs"], c["max_steps"], True, c["seed"], c["eps"],
+                        "k_rollout_bigq", lanes=(512, 512))
+    for t in range(c["steps"]):
+        rep.advance(t + 1)
+        bad = fx.compare(rck.replay_records(rep), 0, t)
+        assert not bad, bad[:8]

@@ -20,3 +20,15 @@ def test_oracle_matches_reference_random_scenarios(map_size, n0, n1, seed, walls
     assert len(got) == len(ref)
     first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
     assert first_bad is None, "first divergence at step %s" % first_bad
+
+
+def test_oracle_matches_reference_large_map_two_episodes():
+    """256x256 (large-map band mode) with 2000 + 2000 agents, random walls and 'random' placement, 200
+    steps of each of two episodes in one env: the band buffers' move order on a thinning map and the
+    attack-shuffle LCG across the restart (GridWorld.cc:79-89, :437-478, :662-672)."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    ref = _random_scenario(common.REF_LIB, 256, 2000, 2000, 6, 200, 400, episodes=2)
+    got = _random_scenario(common.ORACLE_LIB, 256, 2000, 2000, 6, 200, 400, episodes=2)
+    assert len(got) == len(ref) and len(ref) > 200
+    first_bad = next((i for i, (a, b) in enumerate(zip(got, ref)) if a != b), None)
+    assert first_bad is None, "first divergence at step %s" % first_bad

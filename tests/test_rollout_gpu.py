@@ -3,6 +3,8 @@
 Every env of the batch is replayed on the oracle with the actions the on-device policy
 chose; observations (views + features), rewards, mean actions (former_act_prob) and the
 episode restart at max_steps must match bit for bit."""
+import os
+
 import numpy as np
 import pytest
 
@@ -368,6 +370,58 @@ def test_rollout_bigq_bench_shape_matches_oracle():
     eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
     eng.rollout_substeps(S)
     _check_launches(eng, 256, 2048, _sample_envs(E, 8), T, S, max_steps, seed, 0.2, "k_rollout_bigq")
+
+
+@pytest.mark.parametrize("E,S", [(2048, 20), (1, 1)])
+def test_rollout_bigq_matches_reference_recording(E, S):
+    """k_rollout_bigq against the REFERENCE engine's own recording (tests/golden/battle256_rollout.npz,
+    make_battle_fixtures.py): env 0 of the 256x256 batch (2048 + 2048 agents, device rush policy, seed
+    1234) through two full 400-step episodes -- the late-game band order, clear_dead churn, the restart
+    and the LCG across it.  (2048, 20): the bench's batch and launch shape, compared at every launch
+    boundary; (1, 1): one env, compared after every step."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    fx = rck.RolloutFixture()
+    c = fx.case
+    assert E in (1, c["n_envs"])          # env 0 starts at episode length 0 for any batch size
+    eng = BattleBatch(c["map_size"], E, stream=torch.cuda.current_stream())
+    eng.rollout_init(fx.placement, max_steps=c["max_steps"], eps=c["eps"], seed=c["seed"], stagger=True)
+    eng.rollout_substeps(S)
+    assert eng.rollout_path() == "k_rollout_bigq", eng.rollout_path()
+    assert eng.rollout_sum_lanes(65) == 512           # the recording's reward sums are in 512-lane order
+    t = 0
+    while t < c["steps"]:
+        k = min(S, c["steps"] - t)
+        eng.rollout_step(k)
+        t += k
+        eng.rollout_check()
+        bad = fx.compare(rck.device_records(eng, [0]), 0, t - 1)
+        assert not bad, bad[:8]
+    assert fx.restart.sum() == 2
+
+
+def test_rollout_bigq_bench_shape_matches_reference_build():
+    """The 256x256 bench batch (2048 staggered envs, 20 steps per launch, 420 steps) with 4 sampled envs
+    replayed on the reference engine itself (oracle/_ref, one thread) instead of the C oracle."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    if not os.path.exists(common.REF_LIB):
+        pytest.skip("oracle/_ref not built")
+    E, T, S, max_steps, seed = 2048, 420, 20, 400, 1234
+    left, right = bd.block_positions(256, 2048)
+    eng = BattleBatch(256, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.2, seed=seed, stagger=True)
+    eng.rollout_substeps(S)
+    assert eng.rollout_path() == "k_rollout_bigq"
+    chk = rck.RolloutChecker(eng, 256, [left, right], [1, 700, 1500, E - 1], max_steps, True, seed, 0.2,
+                             lib=common.REF_LIB)
+    t = 0
+    while t < T:
+        eng.rollout_step(S)
+        t += S
+        bad = chk.check(t)
+        assert not bad, bad[:8]
+    assert all(r.stats[0] >= 1 for r in chk.replays)
 
 
 def test_rollout_large_env_staggered_many_envs_matches_oracle():
