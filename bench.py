@@ -76,14 +76,15 @@ def parse(argv=None):
     ap.add_argument("--backend", default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher self-test only
-    ap.add_argument("--policy", choices=("rush", "qnet"), default="rush",
+    ap.add_argument("--policy", choices=("rush", "qnet", "mfac"), default="rush",
                     help="rush: the on-device synthetic policy (the metric); qnet: two random-init mean-field Q "
-                         "networks (ValueNet, algo/base.py:123-183) on the HIP forward, one per group")
+                         "networks (ValueNet, algo/base.py:123-183) on the HIP forward, one per group; mfac: two "
+                         "random-init MFAC actor-critic networks (algo/ac.py:219-276) on the HIP forward + draw")
     ap.add_argument("--check-envs", type=int, default=8,
                     help="envs per rank replayed on the C oracle after the timed region (0: no check)")
     a = ap.parse_args(argv)
-    if a.envs is None and a.total_envs is None and a.policy == "qnet":
-        a.envs = 8192                 # the Q-network forward bounds this mode (3.4 MFLOP per agent-step)
+    if a.envs is None and a.total_envs is None and a.policy != "rush":
+        a.envs = 8192                 # the network forward bounds these modes (1.2 / 3.4 MFLOP per agent-step)
     if a.envs is None and a.total_envs is None:
         # 64x64: 131072 envs per GPU (~160 GB of observation buffers, 56 % of the HBM) -- a launch has a fixed
         # cost (ramp-up and the tail of the persistent grid: the last env of each of 1280 workgroups), amortised
@@ -310,20 +311,22 @@ def run_check(eng, args, E, placement, seed, world):
 # ----------------------------------------------------------------------------- learned policy
 QNET_FLOP_PER_AGENT = 2 * (121 * 32 * 63 + 81 * 32 * 288 + 2592 * 256 + 34 * 32 + 21 * 64 + 64 * 32 + 320 * 128 +
                            128 * 64 + 64 * 21)          # 3,417,920: the mean-field QNet forward of one agent
+ACNET_FLOP_PER_AGENT = 2 * (1183 * 256 + 34 * 256 + 512 * 512 + 512 * 21)   # 1,168,896: the AC / MFAC policy path
 F32_MFMA_PEAK_TFS = 157.3                               # MI355X_MICROARCH.md (f32-input MFMA = the f32 VALU rate)
 
 
 def main_qnet(args):
-    """One process, one GPU: a learned policy in the loop (--policy qnet).  Per step: the HIP Q-network
-    forward of each group's model on the observation in the rollout buffers (mfx_qnet_act_rollout), then
-    one k_rollout launch that acts with those actions, steps and observes (mfx_battle_rollout_policy_step).
-    Random-init mean-field QNets (torch modules, packed once); the value counts agent-steps as the rush
-    line does.  The roofline is the forward's: f32 MFMA FLOPs over the two forwards' HIP-event time."""
+    """One process, one GPU: a learned policy in the loop (--policy qnet / mfac).  Per step: the HIP forward
+    of each group's model on the observation in the rollout buffers (mfx_qnet_act_rollout: greedy Q;
+    mfx_acnet_act_rollout: the MFAC policy and its draw), then one k_rollout launch that acts with those actions,
+    steps and observes (mfx_battle_rollout_policy_step).  Random-init networks (torch modules, packed once); the
+    value counts agent-steps as the rush line does.  The roofline is the forward's: f32 MFMA FLOPs over the two
+    forwards' HIP-event time."""
     import torch
     import battle_driver as bd
-    from mfrl_amd.algo.nets import QNet
+    from mfrl_amd.algo.nets import ACNet, QNet
     from mfrl_amd.battle import BattleBatch
-    from mfrl_amd.policy import QNetHIP
+    from mfrl_amd.policy import ACNetHIP, QNetHIP
     torch.cuda.set_device(0)
     E = args.envs if args.total_envs is None else args.total_envs
     stream = torch.cuda.current_stream()
@@ -333,9 +336,14 @@ def main_qnet(args):
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.0, seed=1234)
     torch.manual_seed(7)
     pols = []
+    ac = args.policy == "mfac"
     for g in range(2):
-        net = QNet((13, 13, 7), (34,), 21, True).cuda()
-        pols.append(QNetHIP((13, 13, 7), (34,), 21, True).load(net))
+        if ac:
+            pols.append(ACNetHIP((13, 13, 7), (34,), 21, True).load(ACNet((13, 13, 7), (34,), 21, use_mf=True).cuda()))
+        else:
+            pols.append(QNetHIP((13, 13, 7), (34,), 21, True).load(QNet((13, 13, 7), (34,), 21, True).cuda()))
+    flop_per_agent = ACNET_FLOP_PER_AGENT if ac else QNET_FLOP_PER_AGENT
+    step_no = [0]
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
 
     def agent_steps():
@@ -346,7 +354,11 @@ def main_qnet(args):
         if evs:
             evs[0].record(stream)
         for g in range(2):
-            pols[g].act_rollout(eng, g)
+            if ac:
+                pols[g].act_rollout(eng, g, 1234, step_no[0])
+            else:
+                pols[g].act_rollout(eng, g)
+        step_no[0] += 1
         if evs:
             evs[1].record(stream)
         eng.rollout_policy_step()
@@ -366,19 +378,21 @@ def main_qnet(args):
     units = float((agent_steps() - a0).item())
     fwd_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     eng.rollout_check()
-    flops = QNET_FLOP_PER_AGENT * units / args.steps
-    line = {"metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents, learned MF-Q policy (HIP QNet forward)"
-                      % (args.map, args.map, args.agents),
+    flops = flop_per_agent * units / args.steps
+    what = ("learned MFAC policy (HIP actor-critic forward + draw)" if ac else
+            "learned MF-Q policy (HIP QNet forward)")
+    line = {"metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents, %s" % (args.map, args.map, args.agents,
+                                                                                     what),
             "value": units / (t1 - t0), "unit": "agent-steps/s", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * (t1 - t0) / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (random-init networks)",
-            "config": {"workload": "Battle %dx%d, %d envs, two mean-field QNets (one per group), forward + "
-                                   "fused step per step" % (args.map, args.map, E), "envs_per_gpu": E,
-                       "policy": "qnet"},
+            "config": {"workload": "Battle %dx%d, %d envs, two %s (one per group), forward + fused step per step"
+                                   % (args.map, args.map, E, "MFAC networks" if ac else "mean-field QNets"),
+                       "envs_per_gpu": E, "policy": args.policy},
             "roofline": {"bound": "mfma", "achieved": flops / (fwd_ms * 1e-3) / 1e12, "peak": F32_MFMA_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": flops / (fwd_ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS,
-                         "traffic": None, "kernel": "k_qnet_conv + k_qnet_head (x2 groups)",
-                         "kernel_ms": fwd_ms, "flop_per_unit": QNET_FLOP_PER_AGENT,
+                         "traffic": None, "kernel": "k_acnet (x2 groups)" if ac else "k_qnet_conv + k_qnet_head (x2 groups)",
+                         "kernel_ms": fwd_ms, "flop_per_unit": flop_per_agent,
                          "units_per_step": units / args.steps}}
     print(json.dumps(line), flush=True)
     return 0
@@ -395,7 +409,7 @@ def main():
     if args.launcher_selftest:
         launcher_selftest(args)
         return 0
-    if args.policy == "qnet":
+    if args.policy != "rush":
         return main_qnet(args)
     import torch
     import torch.distributed as dist

@@ -185,6 +185,29 @@ int mfx_qnet_forward(void *handle, const float *d_view, const float *d_feat, con
 int mfx_qnet_act_rollout(void *handle, const float *d_view, const float *d_feat, const int32_t *d_counts,
                          const double *d_mean, int mean_stride, int E, int G, int g, int rowcap, int32_t *d_rows,
                          int32_t *d_total, int32_t *d_act, void *stream);
+/* (the row count stays on the device: the kernels are launched for E * rowcap rows and read *d_total) */
+
+/* The actor-critic network of ActorCritic._create_network (algo/ac.py:48-98) / MFAC._create_network (:219-276)
+ * and its act, tf.multinomial(log(policy)) (:43-46, :213-217), forward only, f32 MFMA
+ * (csrc/acnet_kernels.hip); views of view_floats <= 4096 floats (flattened NHWC), features <= 256,
+ * 2 <= n_action <= 32.  Weights: one float32 blob in the layout mfx_acnet_blob_size reports (19 offsets: wv bv
+ * we be wd0 wd1 bd wp bp wval bval wep bep wdp bdp wvd bvd wvo bvo, every matrix [K][N] row-major, K padded to
+ * 4; the 512-wide dense layer split by output halves).  The draw of row r of group g at step t is the first
+ * action whose running f32 sum of the clipped policy exceeds u * (its f32 total), u = a 24-bit counter hash of
+ * (seed, t, g, r) (tests/acnet_ref.py restates it). */
+int mfx_acnet_blob_size(int view_floats, int feature, int n_action, int use_mf, size_t *n_floats, size_t *offsets);
+int mfx_acnet_create(int view_floats, int feature, int n_action, int use_mf, void **handle);
+int mfx_acnet_destroy(void *handle);
+int mfx_acnet_set_weights(void *handle, const float *d_blob, size_t n_floats, void *stream);
+/* n agents: view [n][view_floats], feature [n][F], prob [n][A] float32 (the MF value head; else null) ->
+ * policy [n][A], value [n], act [n] (each may be null); row i drawn with (seed, step, group 0, row i) */
+int mfx_acnet_forward(void *handle, const float *d_view, const float *d_feat, const float *d_prob, int n,
+                      float *d_policy, float *d_value, int32_t *d_act, uint32_t seed, uint32_t step, void *stream);
+/* group g of a rollout batch -> sampled actions in the rollout's action buffer (live rows; row j of env e drawn
+ * with (seed, step, g, e * rowcap + j)); d_rows: E * rowcap + 1 ints scratch; nothing is read back */
+int mfx_acnet_act_rollout(void *handle, const float *d_view, const float *d_feat, const int32_t *d_counts, int E,
+                          int G, int g, int rowcap, int32_t *d_rows, int32_t *d_total, int32_t *d_act, uint32_t seed,
+                          uint32_t step, void *stream);
 
 /* ---------------------------------------------------------------- part 6: replay rows */
 /* The data path of the replay buffers (algo/tools.py:26-362): for i < n, row idx[i] (or i; modulo src_mod

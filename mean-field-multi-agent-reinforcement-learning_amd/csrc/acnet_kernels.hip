@@ -1,0 +1,323 @@
+// acnet_kernels.hip -- the reference's actor-critic network (ActorCritic._create_network, algo/ac.py:48-98, and
+// MFAC._create_network, :219-276) and its act (tf.multinomial over log(policy), :43-46 / :213-217), forward only,
+// hand-written for gfx950 on the f32-input MFMA v_mfma_f32_16x16x4_f32.  Per agent:
+//
+//   view [V] (flattened NHWC, V = 1,183 at 13 x 13 x 7) --dense 256, relu--> h_view
+//   feature [F]                                        --dense 256, relu--> h_emb
+//   concat(h_view, h_emb) [512] --dense 512, relu--> d
+//   policy = clip(softmax(dense(d / 0.1) -> A), 1e-10, 1 - 1e-10);  act ~ multinomial(log policy)
+//   value (AC):   dense(d -> 1)
+//   value (MFAC): prob [A] --dense 64, relu--> --dense 32, relu--> p;  dense(relu(dense(concat(h_view, h_emb, p)
+//                 [544] -> 256)) -> 1)
+//
+// The policy path is 1.17 MFLOP per agent (dense-view 52 %, dense-512 45 %): MFMA-bound at the f32 matrix rate
+// (157 TF/s).  One kernel, k_acnet: four waves x 16 agents per workgroup, every layer transposed (weights as the
+// A operand, staged in 16-row chunks in LDS and shared by the four waves; the layer's accumulators are the next
+// layer's B operand in registers, policy_gemm.h).  The 512-wide layer is computed as two 256-unit halves, each
+// folded into the policy logits (and the AC value) as soon as it is ready, so at most 3 x 256 activations per
+// agent are live: h_view and h_emb (the concat) and one half of d.
+//
+// The draw: the reference samples tf.multinomial(log(policy)), i.e. action a with probability policy[a] /
+// sum(policy).  Here u = a counter hash of (seed, step, group, row) -> [0, 1) (24 bits), and the action is the
+// first a whose running f32 sum of policy[0..a] exceeds u * sum(policy) (the sums in action order) -- a pure
+// function of the policy row and the counters, restated on the host by tests/acnet_ref.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "mfx_common.h"
+#include "policy_gemm.h"
+#include "../../include/magent_amd.h"
+
+namespace mfx {
+
+constexpr int kAH = 256;                 // hidden width (hidden_size[0])
+constexpr int kAMaxA = 32;               // policy columns (n_action padded)
+constexpr int kAMaxV = 4096;             // flattened view floats the kernel takes
+constexpr int kABlocks = 19;
+
+// Packed weights (every matrix [K][N] row-major, K padded to a multiple of 4 with zero rows):
+//  0 wv  [Vp][256]  h_view          1 bv [256]
+//  2 we  [Fp][256]  h_emb           3 be [256]
+//  4 wd0 [512][256] dense, units 0..255     5 wd1 [512][256] units 256..511     6 bd [512]
+//  7 wp  [512][32]  policy (A columns, zero-padded)                              8 bp [32]
+//  9 wval [512][16] AC value (column 0)                                          10 bval [16]
+// 11 wep [Ap][64]  MF emb_prob      12 bep [64]
+// 13 wdp [64][32]  MF dense_prob    14 bdp [32]
+// 15 wvd [544][256] MF value dense  16 bvd [256]
+// 17 wvo [256][16] MF value (column 0)                                           18 bvo [16]
+// (blocks 9-10 are empty with mean field, 11-18 without.)
+struct ACNetDev {
+    const float* w[kABlocks];
+    int V, Vp, F, Fp, A, Ap, use_mf;
+};
+
+__device__ __forceinline__ uint32_t ac_mix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
+// The uniform of row `row` of group g at step `step` (tests/acnet_ref.py restates it).
+__device__ __forceinline__ float ac_uniform(uint32_t seed, uint32_t step, int g, int row) {
+    const uint32_t k = seed ^ ac_mix32(step * 0x9E3779B9u + (uint32_t)g * 0x632BE5ABu) ^
+                       ac_mix32((uint32_t)row * 0x85EBCA77u + 0x165667B1u);
+    return (float)(ac_mix32(k) >> 8) * (1.0f / 16777216.0f);
+}
+
+// rows (rm.rows): compact agent i -> view / feature row; the action slot as in QRowMap; the prob row of
+// the env (mean field).  d_n: the row count on the device (launch sized for n).  policy_out [n][A],
+// value_out [n], act_out: any may be null.
+template <typename PT, bool kMF>
+__global__ void __launch_bounds__(256, 1) k_acnet(ACNetDev p, const float* __restrict__ view, size_t view_ld,
+                                                  const float* __restrict__ feat, size_t feat_ld,
+                                                  const PT* __restrict__ prob, size_t prob_ld, QRowMap rm, int n,
+                                                  const int32_t* __restrict__ d_n, float* __restrict__ policy_out,
+                                                  float* __restrict__ value_out, int32_t* __restrict__ act_out,
+                                                  uint32_t seed, uint32_t step, int group) {
+    extern __shared__ __attribute__((aligned(16))) float qsm[];
+    if (d_n) n = min(*d_n, n);
+    if ((int)blockIdx.x * kQHeadWaves * 16 >= n) return;           // (uniform: a launch sized for the upper bound)
+    float* bsm = qsm;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
+    const int base = (blockIdx.x * kQHeadWaves + wid) * 16;
+    const int ia = min(base + c, n - 1);                            // this lane's agent (clamped: junk, never written)
+    const int row = rm.rows ? rm.rows[ia] : ia;
+    const int env = rm.rows ? row / rm.rowcap : ia;
+    const float* const* W = p.w;
+    // ---- h_view^T [256 x 16]: view floats k = 16 ch + 4 h + s of this lane's agent, two chunks ahead in flight
+    f32x4 hv[16];
+    {
+        const float* vr = view + (size_t)row * view_ld + 4 * h;
+        const int V = p.V;
+        float b0[4], b1[4], b2[4];
+        auto fetch = [&](int ch, float* b) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = 16 * ch + 4 * h + s;
+                b[s] = k < V ? vr[16 * ch + s] : 0.f;
+            }
+        };
+        fetch(0, b0);
+        fetch(1, b1);
+        int have = -1;
+        wg_gemm_t<16>(W[0], p.Vp, [&](int ch, int s) {
+            if (s == 0 && have != ch) {                             // rotate: chunk ch in b0, ch + 1 in b1
+                if (have >= 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { b0[j] = b1[j]; b1[j] = b2[j]; }
+                }
+                have = ch;
+                fetch(ch + 2, b2);
+            }
+            return b0[s];
+        }, bsm, hv);
+    }
+    // ---- h_emb^T [256 x 16]
+    f32x4 he[16];
+    {
+        const float* fr = feat + (size_t)row * feat_ld;
+        const int F = p.F;
+        wg_gemm_t<16>(W[2], p.Fp, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < F ? fr[k] : 0.f; },
+                      bsm, he);
+    }
+    // concat unit k = 16 ch + 4 h + s: ch < 16 h_view tile ch, else h_emb tile ch - 16
+    auto concat_at = [&](int ch, int s) {
+        return ch < 16 ? relu_unit(hv, W[1], ch, s) : relu_unit(he, W[3], ch - 16, s);
+    };
+    // ---- dense [512] in two halves, each folded into the policy logits (and the AC value) at once
+    f32x4 pl[2];
+    f32x4 vv[1] = {{0.f, 0.f, 0.f, 0.f}};
+    {
+        f32x4 dh[16];
+        wg_gemm_t<16, 32>(W[4], 2 * kAH, concat_at, bsm, dh);
+        wg_gemm_t<2, 16, true>(W[7], kAH, [&](int ch, int s) { return relu_unit(dh, W[6], ch, s) / 0.1f; }, bsm, pl);
+        if (!kMF && value_out)
+            wg_gemm_t<1, 16, true>(W[9], kAH, [&](int ch, int s) { return relu_unit(dh, W[6], ch, s); }, bsm, vv);
+        wg_gemm_t<16, 32>(W[5], 2 * kAH, concat_at, bsm, dh);
+        wg_gemm_t<2, 16, false>(W[7] + kAH * kAMaxA, kAH,
+                                [&](int ch, int s) { return relu_unit(dh, W[6] + kAH, ch, s) / 0.1f; }, bsm, pl);
+        if (!kMF && value_out)
+            wg_gemm_t<1, 16, false>(W[9] + kAH * 16, kAH, [&](int ch, int s) { return relu_unit(dh, W[6] + kAH, ch, s); },
+                                    bsm, vv);
+    }
+    // ---- MF value: emb_prob 64, dense_prob 32, dense 256 over concat(h_view, h_emb, p), value 1
+    if (kMF && value_out) {
+        const PT* pr = prob + (size_t)env * prob_ld;
+        const int A = p.A;
+        f32x4 e1[4], e2[2];
+        wg_gemm_t<4>(W[11], p.Ap, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < A ? (float)pr[k] : 0.f; },
+                     bsm, e1);
+        wg_gemm_t<2, 4>(W[13], 64, [&](int ch, int s) { return relu_unit(e1, W[12], ch, s); }, bsm, e2);
+        f32x4 vd[16];
+        wg_gemm_t<16, 34>(W[15], 2 * kAH + 32, [&](int ch, int s) {
+            return ch < 32 ? concat_at(ch, s) : relu_unit(e2, W[14], ch - 32, s);
+        }, bsm, vd);
+        wg_gemm_t<1, 16>(W[17], kAH, [&](int ch, int s) { return relu_unit(vd, W[16], ch, s); }, bsm, vv);
+    }
+    const int i = base + c;
+    if (value_out && h == 0 && i < n) value_out[i] = vv[0][0] + W[kMF ? 18 : 10][0];   // unit 0: lanes h == 0, r 0
+    // ---- policy: logits of agent c, actions 16 t + 4 h + r, through LDS to lane c of the wave (h == 0): softmax,
+    // clip, the draw
+    float* lg = bsm + wid * 16 * kAMaxA;                             // (the staging buffer is free: wg_gemm_t ended
+#pragma unroll                                                       //  with a barrier)
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lg[c * kAMaxA + 16 * t + 4 * h + r] = pl[t][r];
+    qwave_sync();
+    if (h == 0 && i < n) {
+        const int A = p.A;
+        const float* bp = W[8];
+        float x[kAMaxA];
+        float m = -__builtin_huge_valf();
+#pragma unroll
+        for (int a = 0; a < kAMaxA; ++a) {
+            x[a] = a < A ? lg[c * kAMaxA + a] + bp[a] : 0.f;
+            if (a < A) m = fmaxf(m, x[a]);
+        }
+        float sum = 0.f;
+#pragma unroll
+        for (int a = 0; a < kAMaxA; ++a)
+            if (a < A) { x[a] = expf(x[a] - m); sum += x[a]; }
+        float tot = 0.f;
+#pragma unroll
+        for (int a = 0; a < kAMaxA; ++a)
+            if (a < A) { x[a] = fminf(fmaxf(x[a] / sum, 1e-10f), 1.0f - 1e-10f); tot += x[a]; }
+        if (policy_out) {
+            float* po = policy_out + (size_t)i * A;
+            for (int a = 0; a < A; ++a) po[a] = x[a];
+        }
+        if (act_out) {
+            const float thr = ac_uniform(seed, step, group, row) * tot;
+            float run = 0.f;
+            int pick = -1;
+#pragma unroll
+            for (int a = 0; a < kAMaxA; ++a)
+                if (a < A) {
+                    run += x[a];
+                    if (pick < 0 && run > thr) pick = a;
+                }
+            if (pick < 0) pick = A - 1;                             // (rounding: u * tot at the very top)
+            const size_t slot = rm.rows ? (size_t)(row / rm.rowcap) * rm.act_env + rm.act_off + row % rm.rowcap : (size_t)i;
+            act_out[slot] = pick;
+        }
+    }
+}
+
+}  // namespace mfx
+
+// ------------------------------------------------------------------------------------------ C ABI
+using namespace mfx;
+
+namespace {
+struct ACNetHandle {
+    ACNetDev dev{};
+    float* blob = nullptr;
+    size_t blob_n = 0;
+};
+
+void acnet_sizes(int V, int F, int A, int use_mf, size_t* sz) {
+    const size_t Vp = (V + 3) & ~3, Fp = (F + 3) & ~3, Ap = (A + 3) & ~3;
+    const size_t mf = use_mf ? 1 : 0, ac = 1 - mf;
+    const size_t s[kABlocks] = {Vp * kAH, kAH, Fp * kAH, kAH, 2 * kAH * kAH, 2 * kAH * kAH, 2 * kAH,
+                                2 * kAH * kAMaxA, kAMaxA, ac * 2 * kAH * 16, ac * 16,
+                                mf * Ap * 64, mf * 64, mf * 64 * 32, mf * 32, mf * (2 * kAH + 32) * kAH, mf * kAH,
+                                mf * kAH * 16, mf * 16};
+    for (int k = 0; k < kABlocks; ++k) sz[k] = s[k];
+}
+}  // namespace
+
+extern "C" {
+
+MFX_API int mfx_acnet_blob_size(int view_floats, int feature, int n_action, int use_mf, size_t* n_floats,
+                                size_t* offsets) {
+    if (view_floats < 1 || view_floats > kAMaxV || feature < 1 || feature > 256 || n_action < 2 || n_action > kAMaxA)
+        return fail("acnet: view 1..%d floats, feature 1..256, n_action 2..%d", kAMaxV, kAMaxA);
+    size_t sz[kABlocks], o = 0;
+    acnet_sizes(view_floats, feature, n_action, use_mf, sz);
+    for (int k = 0; k < kABlocks; ++k) {
+        if (offsets) offsets[k] = o;
+        o += (sz[k] + 3) & ~(size_t)3;
+    }
+    *n_floats = o;
+    return 0;
+}
+
+MFX_API int mfx_acnet_create(int view_floats, int feature, int n_action, int use_mf, void** handle) {
+    size_t n = 0, off[kABlocks];
+    MFX_CHECK(mfx_acnet_blob_size(view_floats, feature, n_action, use_mf, &n, off));
+    auto* q = new ACNetHandle();
+    if (hipMalloc(&q->blob, n * sizeof(float)) != hipSuccess) { delete q; return fail("acnet: hipMalloc of %zu floats", n); }
+    q->blob_n = n;
+    for (int k = 0; k < kABlocks; ++k) q->dev.w[k] = q->blob + off[k];
+    q->dev.V = view_floats; q->dev.Vp = (view_floats + 3) & ~3;
+    q->dev.F = feature; q->dev.Fp = (feature + 3) & ~3;
+    q->dev.A = n_action; q->dev.Ap = (n_action + 3) & ~3;
+    q->dev.use_mf = use_mf ? 1 : 0;
+    *handle = q;
+    return 0;
+}
+
+MFX_API int mfx_acnet_destroy(void* handle) {
+    auto* q = static_cast<ACNetHandle*>(handle);
+    if (!q) return 0;
+    if (q->blob) (void)hipFree(q->blob);
+    delete q;
+    return 0;
+}
+
+MFX_API int mfx_acnet_set_weights(void* handle, const float* d_blob, size_t n_floats, void* stream) {
+    auto* q = static_cast<ACNetHandle*>(handle);
+    if (n_floats != q->blob_n) return fail("acnet_set_weights: %zu floats, the layout has %zu", n_floats, q->blob_n);
+    MFX_HIP(hipMemcpyAsync(q->blob, d_blob, n_floats * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+static int acnet_run(ACNetHandle* q, const float* view, size_t view_ld, const float* feat, size_t feat_ld,
+                     const void* prob, int prob_f64, size_t prob_ld, QRowMap rm, int n, const int32_t* d_n,
+                     float* policy, float* value, int32_t* act, uint32_t seed, uint32_t step, int group, hipStream_t st) {
+    if (n <= 0) return 0;
+    if (q->dev.use_mf && value && !prob) return fail("acnet: the mean-field value head needs prob");
+    const int grid = (n + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
+    if (q->dev.use_mf) {
+        if (prob_f64)
+            k_acnet<double, true><<<grid, 256, kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld,
+                                                                 static_cast<const double*>(prob), prob_ld, rm, n, d_n,
+                                                                 policy, value, act, seed, step, group);
+        else
+            k_acnet<float, true><<<grid, 256, kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld,
+                                                                static_cast<const float*>(prob), prob_ld, rm, n, d_n,
+                                                                policy, value, act, seed, step, group);
+    } else {
+        k_acnet<float, false><<<grid, 256, kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld, nullptr, 0, rm, n,
+                                                             d_n, policy, value, act, seed, step, group);
+    }
+    MFX_HIP(hipGetLastError());
+    return 0;
+}
+
+// n agents, dense rows: view [n][V], feature [n][F], prob [n][A] float32 (the MF value head; else null).
+// policy [n][A], value [n], act [n]: any may be null.  The draw of row i uses (seed, step, group 0, row i).
+MFX_API int mfx_acnet_forward(void* handle, const float* d_view, const float* d_feat, const float* d_prob, int n,
+                              float* d_policy, float* d_value, int32_t* d_act, uint32_t seed, uint32_t step,
+                              void* stream) {
+    auto* q = static_cast<ACNetHandle*>(handle);
+    QRowMap rm{nullptr, 1, 0, 0};
+    return acnet_run(q, d_view, q->dev.V, d_feat, q->dev.F, d_prob, 0, q->dev.A, rm, n, nullptr, d_policy, d_value,
+                     d_act, seed, step, 0, (hipStream_t)stream);
+}
+
+// Group g of a rollout batch (as mfx_qnet_act_rollout): sampled actions into d_act [E][G][rowcap] for the group's
+// live rows, row j of env e drawn with (seed, step, g, e * rowcap + j).  Nothing is read back.
+MFX_API int mfx_acnet_act_rollout(void* handle, const float* d_view, const float* d_feat, const int32_t* d_counts,
+                                  int E, int G, int g, int rowcap, int32_t* d_rows, int32_t* d_total, int32_t* d_act,
+                                  uint32_t seed, uint32_t step, void* stream) {
+    auto* q = static_cast<ACNetHandle*>(handle);
+    hipStream_t st = (hipStream_t)stream;
+    MFX_HIP(launch_rollout_rows(d_counts, E, G, g, rowcap, d_rows, d_total, st));
+    QRowMap rm{d_rows, rowcap, G * rowcap, g * rowcap};
+    return acnet_run(q, d_view, q->dev.V, d_feat, q->dev.F, nullptr, 0, 0, rm, E * rowcap, d_total, nullptr, nullptr,
+                     d_act, seed, step, g, st);
+}
+
+}  // extern "C"

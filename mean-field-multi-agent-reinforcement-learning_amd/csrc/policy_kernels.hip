@@ -27,11 +27,11 @@
 #include <algorithm>
 
 #include "mfx_common.h"
+#include "policy_gemm.h"
 #include "../../include/magent_amd.h"
 
 namespace mfx {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kQVH = 13, kQVW = 13, kQNC = 7;           // Battle view (13 x 13 x 7)
 constexpr int kQViewF = kQVH * kQVW * kQNC;             // 1,183
@@ -48,14 +48,6 @@ struct QNetDev {
     int F, Fp, A, Ap, use_mf, Kc;   // Kc: Dense2 input width (288, or 320 with mean field)
 };
 
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void qwave_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // ------------------------------------------------------------------------------------------ conv
 // LDS: w1 [64][32] and Conv2's weights transposed, w2t [32][292] (shared), per wave the view [1,184] and
@@ -77,9 +69,13 @@ __device__ __forceinline__ int conv1_koff(int k) {
 }
 
 // rows: view row of compact agent i (null: i); view_ld: floats per view row.  out: [n][2,592].
+// d_n: the row count on the device (null: n); n is then this pass's upper bound and n_off the pass's first row.
 __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __restrict__ view, size_t view_ld,
-                                                      const int32_t* __restrict__ rows, int n, float* __restrict__ out) {
+                                                      const int32_t* __restrict__ rows, int n, float* __restrict__ out,
+                                                      const int32_t* __restrict__ d_n, int n_off) {
     extern __shared__ __attribute__((aligned(16))) float qsm[];
+    if (d_n) n = min(max(*d_n - n_off, 0), n);
+    if (n <= 0) return;
     float* w1 = qsm;
     float* w2 = w1 + kQK1 * kQCh;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
@@ -215,114 +211,16 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
 }
 
 // ------------------------------------------------------------------------------------------ head
-// One workgroup = 4 waves x 16 agents.  Every layer is computed TRANSPOSED, out^T [N_out x 16 agents] =
-// W^T [N_out x K] . in^T [K x 16]: the weights are the A operand (rows = output units on the lane's column
-// index), the layer input the B operand (agents on the lane's column index).  The accumulator tile then has
-// the agents on its lanes and the output units in its registers, which is exactly the B operand the next
-// layer needs -- "an accumulator tile as the next MFMA's operand" (cdna_hip_programming.md): the
-// activations never leave the registers, with the k order inside each 16-row chunk permuted to match
-// (k-step s of chunk t takes units 16 t + 4 h + s, lane group h supplying its register s).  The weights
-// are staged per 16-row chunk in LDS (double buffered, the next chunk in flight in registers) and shared
-// by the four waves; LDS holds nothing else.
-constexpr int kQHeadWaves = 4, kQKC = 16;                // agents per wave = 16; weight rows per chunk
-// A staged row holds lane c's MT weights (units 16 t + c, t < MT) at c * P + t: 16-B reads of consecutive t.
-// P = MT rounded up to 4, + 4 from 8 on (a 16-lane read then spans every bank group twice at most).
-__host__ __device__ constexpr int qhead_p(int mt) { return ((mt + 3) & ~3) + (mt >= 8 ? 4 : 0); }
-constexpr int kQBLd = 16 * qhead_p(kQHObs / 16);         // the widest staged row (Dense-Obs: 320 floats)
-constexpr size_t kQHeadSmem = (size_t)2 * kQKC * kQBLd * 4;
-
-// acc[MT] = W^T . V over K (K a multiple of 4, rows of W past K read as zero).  W: [K][MT * 16] row-major.
-// v_at(ch, s): this lane's B operand for k = 16 ch + 4 h + s (agent = lane & 15).  NCH > 0: the chunk loop
-// is unrolled (K <= 16 NCH), so a v_at that indexes the previous layer's accumulators by ch stays in
-// registers.  Uniform call sites (barriers inside).
-template <int MT, int NCH = 0, class VF>
-__device__ __forceinline__ void wg_gemm_t(const float* __restrict__ W, int K, VF v_at, float* bsm, f32x4* acc) {
-    constexpr int N = MT * 16;                           // staged row width; 16 rows = MT floats per thread
-    const int lane = threadIdx.x & 63, h = lane >> 4, c = lane & 15;
-    const int nchunk = (K + kQKC - 1) / kQKC;
-    float pre[MT];
-    auto load = [&](int ch) {
-#pragma unroll
-        for (int j = 0; j < MT; ++j) {
-            const int q = threadIdx.x + j * 256, r = q / N, col = q - r * N, k = ch * kQKC + r;
-            pre[j] = k < K ? W[(size_t)k * N + col] : 0.f;
-        }
-    };
-    constexpr int P = qhead_p(MT);
-    auto store = [&](float* dst) {
-#pragma unroll
-        for (int j = 0; j < MT; ++j) {
-            const int q = threadIdx.x + j * 256, r = q / N, col = q - r * N;
-            dst[r * kQBLd + (col & 15) * P + (col >> 4)] = pre[j];
-        }
-    };
-    // this lane's MT weights of k-row kr of the staged chunk cur
-    auto read_row = [&](const float* cur, int kr, float* dst) {
-        const float* src = cur + kr * kQBLd + c * P;
-        if constexpr (MT % 4 == 0) {
-#pragma unroll
-            for (int t4 = 0; t4 < MT / 4; ++t4) {
-                const float4 x = reinterpret_cast<const float4*>(src)[t4];
-                dst[4 * t4] = x.x; dst[4 * t4 + 1] = x.y; dst[4 * t4 + 2] = x.z; dst[4 * t4 + 3] = x.w;
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < MT; ++t) dst[t] = src[t];
-        }
-    };
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-    load(0);
-    store(bsm);
-    __syncthreads();
-    auto chunk = [&](int ch) {
-        const float* cur = bsm + (ch & 1) * kQKC * kQBLd;
-        if (ch + 1 < nchunk) load(ch + 1);               // in flight during this chunk's MFMAs
-        // k-step s + 1's MT weights are read from LDS while k-step s's MT MFMAs issue (the compiler alone
-        // waits on each read right before its MFMA)
-        float av[MT], an[MT];
-        read_row(cur, 4 * h, av);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const float v = v_at(ch, s);
-            if (s + 1 < 4) read_row(cur, 4 * h + s + 1, an);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int t = 0; t < MT; ++t) acc[t] = mfma4(av[t], v, acc[t]);
-#pragma unroll
-            for (int t = 0; t < MT; ++t) av[t] = an[t];
-        }
-        if (ch + 1 < nchunk) store(bsm + ((ch + 1) & 1) * kQKC * kQBLd);
-        __syncthreads();
-    };
-    if constexpr (NCH > 0) {
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch)
-            if (ch < nchunk) chunk(ch);
-    } else {
-        for (int ch = 0; ch < nchunk; ++ch) chunk(ch);
-    }
-}
-
-// relu(acc + bias) of unit 16 t + 4 h + s: the B operand of the next layer's chunk t, k-step s.
-__device__ __forceinline__ float relu_unit(const f32x4* acc, const float* __restrict__ bias, int t, int s) {
-    const int h = (threadIdx.x & 63) >> 4;
-    return fmaxf(acc[t][s] + bias[16 * t + 4 * h + s], 0.f);
-}
-
-// Compact agent i -> (view row, action slot, prob row): rows == null: (i, i, i); else row = rows[i]
-// = e * rowcap + j of a rollout buffer, action slot e * act_env + act_off + j, prob row e.
-struct QRowMap {
-    const int32_t* rows;
-    int rowcap, act_env, act_off;
-};
 
 template <typename PT>
 __global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __restrict__ conv, int n,
                                                       const float* __restrict__ feat, size_t feat_ld,
                                                       const PT* __restrict__ prob, size_t prob_ld, QRowMap rm,
-                                                      float* __restrict__ q_out, int32_t* __restrict__ act_out) {
+                                                      float* __restrict__ q_out, int32_t* __restrict__ act_out,
+                                                      const int32_t* __restrict__ d_n, int n_off) {
     extern __shared__ __attribute__((aligned(16))) float qsm[];
+    if (d_n) n = min(max(*d_n - n_off, 0), n);
+    if ((int)blockIdx.x * kQHeadWaves * 16 >= n) return;          // (uniform: a launch sized for the upper bound)
     float* bsm = qsm;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
     const int base = (blockIdx.x * kQHeadWaves + wid) * 16;
@@ -431,6 +329,12 @@ __global__ void __launch_bounds__(1024) k_qnet_rows(const int32_t* __restrict__ 
     if (t == 1023) *total = part[1023];
 }
 
+hipError_t launch_rollout_rows(const int32_t* counts, int E, int G, int g, int rowcap, int32_t* rows, int32_t* total,
+                               hipStream_t st) {
+    k_qnet_rows<<<1, 1024, 0, st>>>(counts, E, G, g, rowcap, rows, total);
+    return hipGetLastError();
+}
+
 }  // namespace mfx
 
 // ------------------------------------------------------------------------------------------ C ABI
@@ -510,9 +414,10 @@ MFX_API int mfx_qnet_set_weights(void* handle, const float* d_blob, size_t n_flo
 // (10 KB per agent: 2.7 GB at this size).
 constexpr int kQPass = 1 << 18;
 
+// n rows (d_n: the count on the device, n its upper bound -- nothing is read back; launches sized for n).
 static int qnet_run(QNetHandle* q, const float* view, size_t view_ld, const float* feat, size_t feat_ld,
                     const void* prob, int prob_f64, size_t prob_ld, QRowMap rm, int n, float* q_out, int32_t* act,
-                    hipStream_t st) {
+                    hipStream_t st, const int32_t* d_n = nullptr) {
     if (n <= 0) return 0;
     if (q->dev.use_mf && !prob) return fail("qnet: the mean-field net needs prob");
     try { q->conv.ensure((size_t)std::min(n, kQPass) * kQFlat); } catch (const HipFailure& f) { return fail("%s", f.what()); }
@@ -532,15 +437,17 @@ static int qnet_run(QNetHandle* q, const float* view, size_t view_ld, const floa
         float* qo = q_out ? q_out + (size_t)off * q->dev.A : nullptr;
         int32_t* ao = act ? (r.rows ? act : act + off) : nullptr;
         const int cgrid = std::min((m + kQConvWaves - 1) / kQConvWaves, cus * 8);
-        k_qnet_conv<<<cgrid, 256, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p);
+        k_qnet_conv<<<cgrid, 256, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p, d_n, off);
         MFX_HIP(hipGetLastError());
         const int hgrid = (m + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
         if (prob_f64)
             k_qnet_head<double><<<hgrid, 256, kQHeadSmem, st>>>(q->dev, q->conv.p, m, f, feat_ld,
-                                                                 static_cast<const double*>(pb), prob_ld, r, qo, ao);
+                                                                 static_cast<const double*>(pb), prob_ld, r, qo, ao,
+                                                                 d_n, off);
         else
             k_qnet_head<float><<<hgrid, 256, kQHeadSmem, st>>>(q->dev, q->conv.p, m, f, feat_ld,
-                                                                static_cast<const float*>(pb), prob_ld, r, qo, ao);
+                                                                static_cast<const float*>(pb), prob_ld, r, qo, ao,
+                                                                d_n, off);
         MFX_HIP(hipGetLastError());
     }
     return 0;
@@ -557,21 +464,18 @@ MFX_API int mfx_qnet_forward(void* handle, const float* d_view, const float* d_f
 
 // Group g of a rollout batch ([E][rowcap] view / feature rows, counts [E][G], former mean actions
 // [E][G][mean_stride] float64): actions into d_act [E][G][rowcap] for the group's live rows.  d_rows:
-// scratch of E * rowcap ints, d_total: one int.  The row list is built on the device; n_max bounds the
-// rows the kernels are launched for (E * rowcap).
+// scratch of E * rowcap ints, d_total: one int.  The row list and its count stay on the device: the kernels
+// are launched for the upper bound E * rowcap and read the count themselves (no host round trip, so the
+// whole act step can be captured in a graph or queued behind the previous launch).
 MFX_API int mfx_qnet_act_rollout(void* handle, const float* d_view, const float* d_feat, const int32_t* d_counts,
                                  const double* d_mean, int mean_stride, int E, int G, int g, int rowcap,
                                  int32_t* d_rows, int32_t* d_total, int32_t* d_act, void* stream) {
     auto* q = static_cast<QNetHandle*>(handle);
     hipStream_t st = (hipStream_t)stream;
-    k_qnet_rows<<<1, 1024, 0, st>>>(d_counts, E, G, g, rowcap, d_rows, d_total);
-    MFX_HIP(hipGetLastError());
-    int total = 0;
-    MFX_HIP(hipMemcpyAsync(&total, d_total, sizeof(int), hipMemcpyDeviceToHost, st));
-    MFX_HIP(hipStreamSynchronize(st));
+    MFX_HIP(launch_rollout_rows(d_counts, E, G, g, rowcap, d_rows, d_total, st));
     QRowMap rm{d_rows, rowcap, G * rowcap, g * rowcap};
     return qnet_run(q, d_view, kQViewF, d_feat, q->dev.F, d_mean + (size_t)g * mean_stride, 1, (size_t)G * mean_stride,
-                    rm, total, nullptr, d_act, st);
+                    rm, E * rowcap, nullptr, d_act, st, d_total);
 }
 
 }  // extern "C"

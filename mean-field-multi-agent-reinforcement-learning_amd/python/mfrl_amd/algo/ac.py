@@ -1,18 +1,21 @@
 """ActorCritic and MFAC of algo/ac.py:8-361 on PyTorch-ROCm.
 
-act samples the clipped softmax policy (tf.multinomial of its log); train builds one batch from the
+act samples the clipped softmax policy (tf.multinomial of its log) on the hand-written HIP forward
+(mfrl_amd.policy.ACNetHIP, csrc/acnet_kernels.hip: the policy and a counter-hash draw, its weights re-packed
+only when training changed them); train builds one batch from the
 episode buffer, bootstraps every agent's sequence from the value of its last row, and runs the
 discounted-return recursion keep = keep * gamma + r on the device (HIP kernel mfx_mfac_returns,
 algo/ac.py:305-320), then one Adam step on pg + value_coef * vf + ent_coef * neg_entropy.
 """
 import os
+import zlib
 
 import numpy as np
 import torch
 
 from .. import mf
 from . import tools
-from .base import as_dev
+from .base import as_dev, weights_key
 from .nets import ACNet
 
 
@@ -37,6 +40,12 @@ class ActorCritic:
         self.replay_buffer = tools.EpisodesBuffer(use_mean=self._use_mf)
         self.net = ACNet(self.view_space, self.feature_space, self.num_actions, use_mf=self._use_mf).cuda()
         self.optimizer = torch.optim.Adam(self.net.parameters(), lr=self.learning_rate)
+        self._hip = None
+        self._hip_key = None
+        self._draws = 0             # act() calls: the step counter of the device draw
+        # the draw's seed: fixed per model name (np.random is left alone -- the reference consumes it in the
+        # replay buffers, and seeded runs must draw the same indices)
+        self.seed = zlib.crc32(("%s/%s" % (self._prefix, name)).encode())
 
     @property
     def vars(self):
@@ -47,8 +56,29 @@ class ActorCritic:
 
     @torch.no_grad()
     def act_dev(self, **kwargs):
-        policy, _ = self.net(as_dev(kwargs["state"][0]), as_dev(kwargs["state"][1]), need_value=False)
+        """Device in, device out: int32 actions drawn from the clipped softmax policy (algo/ac.py:43-46,
+        tf.multinomial(log(policy))) by the HIP forward k_acnet; the draw's uniforms are a counter hash of
+        (self.seed, the act() count, the row) instead of TensorFlow's stream."""
+        view, feat = as_dev(kwargs["state"][0]), as_dev(kwargs["state"][1])
+        if self._hip_ok():
+            self._draws += 1
+            return self._hip_net().act(view, feat, seed=self.seed, step=self._draws)
+        policy, _ = self.net(view, feat, need_value=False)
         return torch.multinomial(policy, 1).reshape(-1).to(torch.int32)
+
+    def _hip_net(self):
+        """The HIP forward with the network's current weights (re-packed only after they changed)."""
+        if self._hip is None:
+            from ..policy import ACNetHIP
+            self._hip = ACNetHIP(self.view_space, self.feature_space, self.num_actions, self._use_mf)
+        key = weights_key(self.net)
+        if key != self._hip_key:
+            self._hip.load(self.net)
+            self._hip_key = key
+        return self._hip
+
+    def _hip_ok(self):
+        return 2 <= self.num_actions <= 32 and int(np.prod(self.view_space)) <= 4096 and self.feature_space[0] <= 256
 
     def act(self, **kwargs):
         return self.act_dev(**kwargs).cpu().numpy().astype(np.int32)
@@ -74,8 +104,12 @@ class ActorCritic:
         reward = rows["rew"].clone()
         prob = rows.get("prob")
         last = torch.cumsum(counts, 0) - 1
-        with torch.no_grad():                     # value of every agent's last row (the bootstrap)
-            _, keep = self.net(view[last], feature[last], prob[last] if prob is not None else None)
+        with torch.no_grad():                     # value of every agent's last row (the bootstrap), on k_acnet
+            if self._hip_ok():
+                _, keep, _ = self._hip_net().forward(view[last], feature[last], prob[last] if prob is not None else None,
+                                                     want_policy=False, want_value=True, want_act=False)
+            else:
+                _, keep = self.net(view[last], feature[last], prob[last] if prob is not None else None)
         offsets = torch.zeros(len(counts) + 1, dtype=torch.int64, device="cuda")
         offsets[1:] = torch.cumsum(counts, 0)
         mf.mfac_returns(reward, offsets, keep.float().contiguous(), self.gamma)

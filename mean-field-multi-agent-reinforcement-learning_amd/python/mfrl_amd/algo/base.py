@@ -19,6 +19,13 @@ def as_dev(x, dtype=torch.float32):
     return torch.as_tensor(np.asarray(x), dtype=dtype, device="cuda")
 
 
+def weights_key(net, gen=0):
+    """Changes whenever `net`'s weights may have changed: every in-place update of a parameter (optimiser
+    steps, copy_, load_state_dict) bumps its version counter; `gen` covers updates torch does not see (a
+    replayed HIP graph).  The HIP forwards re-pack their weight blob only when the key moves."""
+    return (gen, tuple((p.data_ptr(), p._version) for p in net.parameters()))
+
+
 class ValueNet:
     graph_train = True          # train() replays the minibatch step as a HIP graph (train_batches)
 
@@ -46,6 +53,8 @@ class ValueNet:
         # minibatch update (sample gather, target, loss, backward, Adam, soft update) as a HIP graph
         self.optimizer = torch.optim.Adam(self.eval_net.parameters(), lr=self.lr, capturable=True)
         self._graph = None
+        self._wgen = 0              # bumped after graph replays (they update the weights behind torch's back)
+        self._hip_key = None
 
     @property
     def vars(self):
@@ -119,6 +128,7 @@ class ValueNet:
             self._s_nxt.copy_(nxt_d[i])
             self._graph.replay()
             stats[i].copy_(self._s_out)
+        self._wgen += 1
         st = stats.cpu().numpy()
         for i in range(0, batch_num, 50):
             print("[*] LOSS:", float(st[i, 0]), "/ Q:", {"Eval-Q": np.round(float(st[i, 1]), 6)})
@@ -173,7 +183,10 @@ class ValueNet:
             if getattr(self, "_hip", None) is None:
                 from ..policy import QNetHIP
                 self._hip = QNetHIP(self.view_space, self.feature_space, self.num_actions, self.use_mf)
-            self._hip.load(self.eval_net)                # the weights train() last left
+            key = weights_key(self.eval_net, self._wgen)
+            if key != self._hip_key:                     # the weights train() last left, packed once
+                self._hip.load(self.eval_net)
+                self._hip_key = key
             return self._hip.act(view, feat, prob)
         e_q = self.eval_net(view, feat, prob)
         return torch.argmax(torch.softmax(e_q / self.temperature, dim=1), dim=1).to(torch.int32)

@@ -89,3 +89,72 @@ def _episode(rs, n_agents, temperature, steps, lr, act_rate, decay_rate, decay_g
             break
     return {"q": Q, "order": np.array(orders), "n_up": np.array(nups), "actions": np.stack(acts),
             "spins": spins, "steps": len(orders)}
+
+
+def mfq_loop(n_agents, temperature, steps, lr=0.1, act_rate=1.0, decay_rate=0.99, decay_gap=2000, seed=13):
+    """main_MFQ_Ising.py's episode loop (:84-159) restated PER AGENT, as the script runs it -- the CPU baseline
+    of the reference loop (one core), not a faster port: boltzman_explore per agent (:55-67: np.exp per action,
+    list arithmetic, np.random.choice(2, 1, p)), the env step per agent over the dense N-long spin masks
+    (IsingWorld.step, Scenario.reward / observation: core.py:99-116, Ising.py:101-119, each O(N) per agent),
+    and the Q update loop over act_group (:126-133).  The same numpy stream as mfq(), bit for bit
+    (tests/test_ising_cpu.py)."""
+    rs = np.random.RandomState(seed)
+    for _ in range(n_agents):                  # make_world -> reset_world
+        rs.choice(2)
+    np_state = np.random.get_state()
+    np.random.set_state(rs.get_state())        # the script draws from the global numpy stream
+    try:
+        L = int(round(n_agents ** 0.5))
+        spin = [int(np.random.choice(2)) for _ in range(n_agents)]            # env.reset()
+        nbr = neighbours(n_agents)
+        masks = np.zeros((n_agents, n_agents))
+        for i in range(n_agents):
+            masks[i, nbr[i]] = 1.0
+        gstate = np.array(spin, dtype=np.float64).reshape(L, L)
+        obs = [gstate.flatten()[np.where(masks[i] == 1)] for i in range(n_agents)]
+        Q = np.zeros((n_agents, nbr.shape[1] + 1, 2))
+        current_t, max_order, done_ = 0.3, 0.0, 0
+        orders = []
+        for t in range(steps):
+            action = np.zeros(n_agents, dtype=np.int32)
+            if t % decay_gap == 0:
+                current_t *= decay_rate
+            if current_t < temperature:
+                current_t = temperature
+            for i in range(n_agents):
+                obs_flat = np.count_nonzero(obs[i] == 1)
+                nums, denom = [], 0
+                for a in range(2):
+                    val = np.exp(Q[i, obs_flat, a] / current_t)
+                    nums.append(val)
+                    denom += val
+                action[i] = np.random.choice(2, 1, p=[x / denom for x in nums])[0]
+            # IsingMultiAgentEnv._step: spins := actions, then per agent observation and reward (new spins)
+            for i in range(n_agents):
+                gstate[i // L, i % L] = 0 if action[i] == 0 else 1
+            n_up = np.count_nonzero(gstate.flatten())
+            order = abs(n_up - (n_agents - n_up)) / (n_agents + 0.0)
+            obs_, reward = [], []
+            for i in range(n_agents):
+                obs_.append(gstate.flatten()[np.where(masks[i] == 1)])
+                g = gstate.copy()
+                g[np.where(g == 0)] = -1
+                local = -0.5 * g[i // L, i % L] * np.sum(g.flatten() * masks[i])
+                reward.append(-local)
+            act_group = np.random.choice(n_agents, int(act_rate * n_agents), replace=False)
+            for i in act_group:
+                obs_flat = np.count_nonzero(obs[i] == 1)
+                Q[i, obs_flat, action[i]] = Q[i, obs_flat, action[i]] + lr * (reward[i] - Q[i, obs_flat, action[i]])
+            obs = obs_
+            orders.append(order)
+            if order > max_order:
+                max_order = order
+            if abs(max_order - order) < 0.001:
+                done_ += 1
+            else:
+                done_ = 0
+            if done_ == 500:
+                break
+        return {"q": Q, "order": np.array(orders), "steps": len(orders)}
+    finally:
+        np.random.set_state(np_state)

@@ -79,3 +79,15 @@ def test_oracle_episodes_match_reference_fixture():
         assert ep["order"].tobytes() == fx[p + "order"].tobytes()
         np.testing.assert_array_equal(ep["n_up"], fx[p + "n_up"])
         assert ep["q"].tobytes() == fx[p + "q_final"].tobytes()
+
+
+@pytest.mark.parametrize("n,steps", [(100, 40), (400, 6)])
+def test_per_agent_loop_restatement_matches_the_vectorised_oracle(n, steps):
+    """oracle.ising_oracle.mfq_loop (the CPU baseline of the reference's per-agent loop) consumes the same numpy
+    stream and gives the same Q table and order parameters as the vectorised oracle, bit for bit."""
+    import ising_oracle
+    a = ising_oracle.mfq_loop(n, 0.8, steps, seed=13)
+    b = ising_oracle.mfq(n, 0.8, steps, seed=13)
+    assert a["steps"] == b["steps"]
+    assert a["q"].tobytes() == b["q"].tobytes()
+    assert a["order"].tobytes() == b["order"].tobytes()

@@ -199,3 +199,165 @@ def test_learned_policy_rollout_matches_oracle(monkeypatch):
         obs = nxt
     eng.rollout_check()
     assert restarts >= E and checked > 1000
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# the actor-critic forward (ActorCritic / MFAC, algo/ac.py:48-98, :219-276) on k_acnet
+# ---------------------------------------------------------------------------------------------------------------
+def _acnet(use_mf, seed):
+    import torch
+    from mfrl_amd.algo.nets import ACNet
+    torch.manual_seed(seed)
+    net = ACNet((13, 13, 7), (34,), 21, use_mf=use_mf).cuda()
+    with torch.no_grad():
+        for p in net.parameters():
+            p.add_(0.02 * torch.randn_like(p))
+    return net
+
+
+@pytest.mark.parametrize("use_mf", [False, True])
+def test_acnet_forward_matches_torch_module(use_mf):
+    """k_acnet on bench-shape rows (~10^5 live agents of a 64x64 rollout) against the torch ACNet it was packed
+    from: the clipped softmax policy and the value within 1e-5 (scaled by the value's magnitude); a sample of
+    rows against the float64 restatement on the packed blob; every sampled action equals the host restatement of
+    the draw on the kernel's own policy rows.  Parity with TF's network itself is unpinned (TensorFlow absent)."""
+    import acnet_ref
+    import torch
+    from mfrl_amd.policy import ACNetHIP
+    net = _acnet(use_mf, 31 + use_mf)
+    view, feat, prob = _rollout_obs()
+    n = view.shape[0]
+    assert n > 50000
+    hip = ACNetHIP((13, 13, 7), (34,), 21, use_mf).load(net)
+    pol, val, act = hip.forward(view, feat, prob, want_value=True, seed=77, step=5)
+    with torch.no_grad():
+        wp, wv = net(view, feat, prob if use_mf else None)
+    torch.cuda.synchronize()
+    perr = float((pol - wp).abs().max())
+    scale = max(1.0, float(wv.abs().max()))
+    verr = float((val - wv).abs().max())
+    assert perr <= 1e-5, perr
+    assert verr <= 1e-5 * scale, (verr, scale)
+    assert float(wp.max(1).values.mean()) < 0.999            # (a policy that is not one-hot everywhere)
+    want = acnet_ref.draw(pol.cpu().numpy(), 77, 5, 0, np.arange(n))
+    assert np.array_equal(act.cpu().numpy(), want)
+    idx = torch.randperm(n, device="cuda")[:512]
+    rp, rv = acnet_ref.forward(hip.pack(net).cpu().double().numpy(), hip.offsets, 1183, 34, 21, use_mf,
+                               view[idx].cpu().numpy(), feat[idx].cpu().numpy(), prob[idx].cpu().numpy())
+    assert np.abs(pol[idx].cpu().double().numpy() - rp).max() <= 1e-5
+    assert np.abs(val[idx].cpu().double().numpy() - rv).max() <= 1e-5 * scale
+    # the draw follows the policy: mean sampled-action probability against the expected one
+    p_of = pol.gather(1, act.long()[:, None]).squeeze(1)
+    assert abs(float(p_of.mean()) - float((pol * pol).sum(1).mean())) < 0.01
+
+
+def test_acnet_forward_small_and_ragged_batches():
+    """n = 1, 15, 17, 63, 65 give the rows (policy, value, draw) a full batch gives them."""
+    import torch
+    from mfrl_amd.policy import ACNetHIP
+    net = _acnet(True, 9)
+    view, feat, prob = _rollout_obs(E=256, steps=30)
+    hip = ACNetHIP((13, 13, 7), (34,), 21, True).load(net)
+    p_all, v_all, a_all = hip.forward(view[:200], feat[:200], prob[:200], want_value=True, seed=3, step=1)
+    for n in (1, 15, 17, 63, 65):
+        p, v, a = hip.forward(view[:n], feat[:n], prob[:n], want_value=True, seed=3, step=1)
+        torch.cuda.synchronize()
+        assert torch.equal(p, p_all[:n]) and torch.equal(v, v_all[:n]) and torch.equal(a, a_all[:n]), n
+
+
+def test_mfac_policy_rollout_matches_oracle(monkeypatch):
+    """Two MFAC networks (one per group) in the loop on the fused k_rollout: per step mfx_acnet_act_rollout
+    samples every live agent's action on the device from the observation in the rollout buffers (nothing read
+    back), k_rollout (kMode 1) steps with them and observes.  The device's actions equal the host restatement
+    of the draw on the kernel's policy rows for the same observation (row e * rowcap + j, group g, the step);
+    every env is replayed on the C oracle with those actions: views, features, rewards, mean actions bit for
+    bit, restarts included."""
+    import acnet_ref
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    from mfrl_amd.policy import ACNetHIP
+    monkeypatch.setenv("MFX_SMALL_E", "0")
+    E, T, max_steps, VF, F, seed = 3, 70, 30, 1183, 34, 4242
+    left, right = bd.block_positions(64, 128)
+    eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+    eng.rollout_init([left, right], max_steps=max_steps, eps=0.0, seed=1, stagger=False)
+    assert eng.rollout_path() == "k_rollout"
+    pols = [ACNetHIP((13, 13, 7), (34,), 21, True).load(_acnet(True, 40 + g)) for g in range(2)]
+    rc = eng.rowcap
+    oracles = []
+    for e in range(E):
+        env, h = common.battle_env(common.ORACLE_LIB, 64)
+        env.reset()
+        env.add_agents(h[0], method="custom", pos=left)
+        env.add_agents(h[1], method="custom", pos=right)
+        oracles.append([env, h, 0])
+    eng.rollout_policy_observe()
+
+    def grab():
+        out = {}
+        for g in range(2):
+            out["view%d" % g] = torch.empty((E, rc, VF), dtype=torch.float32, device="cuda")
+            out["feat%d" % g] = torch.empty((E, rc, F), dtype=torch.float32, device="cuda")
+            eng.rollout_copy("view", out["view%d" % g], group=g)
+            eng.rollout_copy("feature", out["feat%d" % g], group=g)
+        out["mean"] = torch.empty((E, 2, 21), dtype=torch.float64, device="cuda")
+        eng.rollout_copy("mean_action", out["mean"])
+        eng.sync()
+        return out
+
+    obs = grab()
+    restarts = 0
+    for t in range(T):
+        for g in range(2):
+            pols[g].act_rollout(eng, g, seed, t)
+        act = torch.empty((E, 2, rc), dtype=torch.int32, device="cuda")
+        eng.rollout_copy("actions", act)
+        eng.sync()
+        actn = act.cpu().numpy()
+        for g in range(2):
+            for e in range(E):
+                n = len(oracles[e][0].get_agent_id(oracles[e][1][g]))
+                if not n:
+                    continue
+                pol, _, _ = pols[g].forward(obs["view%d" % g][e, :n], obs["feat%d" % g][e, :n], want_act=False)
+                want = acnet_ref.draw(pol.cpu().numpy(), seed, t, g, e * rc + np.arange(n))
+                assert np.array_equal(actn[e, g, :n], want), (t, e, g)
+        eng.rollout_policy_step()
+        nxt = grab()
+        rew = torch.empty((E, 2, rc), dtype=torch.float32, device="cuda")
+        eng.rollout_copy("rewards", rew)
+        eng.sync()
+        for e, st in enumerate(oracles):
+            env, h, _ = st
+            acts = [np.ascontiguousarray(actn[e, g, :len(env.get_agent_id(h[g]))]) for g in range(2)]
+            for g in range(2):
+                env.set_action(h[g], acts[g])
+            done = env.step()
+            for g in range(2):
+                rw = env.get_reward(h[g])
+                assert rew[e, g, :len(rw)].cpu().numpy().tobytes() == rw.tobytes(), (t, e, g, "reward")
+            env.clear_dead()
+            st[2] += 1
+            restart = done or st[2] >= max_steps
+            for g in range(2):
+                n = len(acts[g])
+                want = np.bincount(acts[g], minlength=21) / n if n else np.full(21, np.nan)
+                got = nxt["mean"][e, g].cpu().numpy()
+                if restart:
+                    assert not got.any(), (t, e, g, "mean reset")
+                else:
+                    assert np.array_equal(got, want, equal_nan=True), (t, e, g, "mean")
+            if restart:
+                st[2] = 0
+                restarts += 1
+                env.reset()
+                env.add_agents(h[0], method="custom", pos=left)
+                env.add_agents(h[1], method="custom", pos=right)
+            for g in range(2):
+                v, f = env.get_observation(h[g])
+                n = len(v)
+                assert nxt["view%d" % g][e, :n].cpu().numpy().tobytes() == v.reshape(n, VF).tobytes(), (t, e, g)
+                assert nxt["feat%d" % g][e, :n].cpu().numpy().tobytes() == f.tobytes(), (t, e, g)
+        obs = nxt
+    eng.rollout_check()
+    assert restarts >= E
