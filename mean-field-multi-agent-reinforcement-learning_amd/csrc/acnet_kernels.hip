@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "mfx_common.h"
@@ -68,8 +70,15 @@ __device__ __forceinline__ float ac_uniform(uint32_t seed, uint32_t step, int g,
 // rows (rm.rows): compact agent i -> view / feature row; the action slot as in QRowMap; the prob row of
 // the env (mean field).  d_n: the row count on the device (launch sized for n).  policy_out [n][A],
 // value_out [n], act_out: any may be null.
-template <typename PT, bool kMF>
-__global__ void __launch_bounds__(256, 1) k_acnet(ACNetDev p, const float* __restrict__ view, size_t view_ld,
+// kHeLds (features of at most kHeF floats, the Battle shape's 34): h_emb is never held.  Its weights sit in LDS for
+// the whole kernel and each 16-unit tile of it is recomputed from the features (9 MFMAs, 9 feature registers) right
+// where the concat needs it -- 3 % more MFMA work for 64 fewer registers per lane, which is what lets two
+// workgroups share a CU (one wave per SIMD otherwise: 256 VGPRs + ~100 AGPRs).
+constexpr int kHeF = 36;
+constexpr size_t kAcnetLdsSmem = kQHeadSmem + (size_t)kHeF * kAH * 4;
+
+template <typename PT, bool kMF, bool kHeLds>
+__global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const float* __restrict__ view, size_t view_ld,
                                                   const float* __restrict__ feat, size_t feat_ld,
                                                   const PT* __restrict__ prob, size_t prob_ld, QRowMap rm, int n,
                                                   const int32_t* __restrict__ d_n, float* __restrict__ policy_out,
@@ -113,33 +122,69 @@ __global__ void __launch_bounds__(256, 1) k_acnet(ACNetDev p, const float* __res
             return b0[s];
         }, bsm, hv);
     }
-    // ---- h_emb^T [256 x 16]
-    f32x4 he[16];
+    // the concat's h_view half, activated in place once (relu(acc + bias)): read as is by every later layer
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[t][r] = relu_unit(hv, W[1], t, r);
+    // ---- h_emb^T [256 x 16]: held (kHeLds false), or recomputed per tile from the LDS-resident weights
+    f32x4 he[kHeLds ? 1 : 16];
+    float fr4[kHeLds ? kHeF / 4 : 1];
+    const float* weS = bsm + 2 * kQKC * kQBLd;                      // kHeLds: We [kHeF][256] after the staging
     {
         const float* fr = feat + (size_t)row * feat_ld;
         const int F = p.F;
-        wg_gemm_t<16>(W[2], p.Fp, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < F ? fr[k] : 0.f; },
-                      bsm, he);
+        if (kHeLds) {
+            float* wd = bsm + 2 * kQKC * kQBLd;
+            for (int i = threadIdx.x; i < kHeF * kAH; i += blockDim.x) wd[i] = i < p.Fp * kAH ? W[2][i] : 0.f;
+#pragma unroll
+            for (int ks = 0; ks < kHeF / 4; ++ks) {                 // k = 4 ks + h: this lane's B operands
+                const int k = 4 * ks + h;
+                fr4[ks] = k < F ? fr[k] : 0.f;
+            }
+            __syncthreads();
+        } else {
+            wg_gemm_t<16>(W[2], p.Fp, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < F ? fr[k] : 0.f; },
+                          bsm, he);
+        }
     }
+    // h_emb tile t (units 16 t + 4 h + r in register r, agent c): A = We^T rows 16 t + c from LDS, B = the features
+    auto he_tile = [&](int t) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < kHeF / 4; ++ks) acc = mfma4(weS[(4 * ks + h) * kAH + 16 * t + c], fr4[ks], acc);
+        return acc;
+    };
+    f32x4 he_cur = {0.f, 0.f, 0.f, 0.f};
     // concat unit k = 16 ch + 4 h + s: ch < 16 h_view tile ch, else h_emb tile ch - 16
     auto concat_at = [&](int ch, int s) {
-        return ch < 16 ? relu_unit(hv, W[1], ch, s) : relu_unit(he, W[3], ch - 16, s);
+        if (ch < 16) return hv[ch][s];
+        if (kHeLds) {
+            if (s == 0) he_cur = he_tile(ch - 16);
+            return relu_unit(&he_cur, W[3] + 16 * (ch - 16), 0, s);
+        }
+        return relu_unit(he, W[3], ch - 16, s);
     };
     // ---- dense [512] in two halves, each folded into the policy logits (and the AC value) at once
     f32x4 pl[2];
     f32x4 vv[1] = {{0.f, 0.f, 0.f, 0.f}};
     {
         f32x4 dh[16];
+        auto act_half = [&](int half) {                             // relu(acc + bias) in place
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dh[t][r] = relu_unit(dh, W[6] + half * kAH, t, r);
+        };
         wg_gemm_t<16, 32>(W[4], 2 * kAH, concat_at, bsm, dh);
-        wg_gemm_t<2, 16, true>(W[7], kAH, [&](int ch, int s) { return relu_unit(dh, W[6], ch, s) / 0.1f; }, bsm, pl);
-        if (!kMF && value_out)
-            wg_gemm_t<1, 16, true>(W[9], kAH, [&](int ch, int s) { return relu_unit(dh, W[6], ch, s); }, bsm, vv);
+        act_half(0);
+        wg_gemm_t<2, 16, true>(W[7], kAH, [&](int ch, int s) { return dh[ch][s] / 0.1f; }, bsm, pl);
+        if (!kMF && value_out) wg_gemm_t<1, 16, true>(W[9], kAH, [&](int ch, int s) { return dh[ch][s]; }, bsm, vv);
         wg_gemm_t<16, 32>(W[5], 2 * kAH, concat_at, bsm, dh);
-        wg_gemm_t<2, 16, false>(W[7] + kAH * kAMaxA, kAH,
-                                [&](int ch, int s) { return relu_unit(dh, W[6] + kAH, ch, s) / 0.1f; }, bsm, pl);
+        act_half(1);
+        wg_gemm_t<2, 16, false>(W[7] + kAH * kAMaxA, kAH, [&](int ch, int s) { return dh[ch][s] / 0.1f; }, bsm, pl);
         if (!kMF && value_out)
-            wg_gemm_t<1, 16, false>(W[9] + kAH * 16, kAH, [&](int ch, int s) { return relu_unit(dh, W[6] + kAH, ch, s); },
-                                    bsm, vv);
+            wg_gemm_t<1, 16, false>(W[9] + kAH * 16, kAH, [&](int ch, int s) { return dh[ch][s]; }, bsm, vv);
     }
     // ---- MF value: emb_prob 64, dense_prob 32, dense 256 over concat(h_view, h_emb, p), value 1
     if (kMF && value_out) {
@@ -279,19 +324,22 @@ static int acnet_run(ACNetHandle* q, const float* view, size_t view_ld, const fl
     if (n <= 0) return 0;
     if (q->dev.use_mf && value && !prob) return fail("acnet: the mean-field value head needs prob");
     const int grid = (n + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
-    if (q->dev.use_mf) {
-        if (prob_f64)
-            k_acnet<double, true><<<grid, 256, kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld,
-                                                                 static_cast<const double*>(prob), prob_ld, rm, n, d_n,
-                                                                 policy, value, act, seed, step, group);
-        else
-            k_acnet<float, true><<<grid, 256, kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld,
-                                                                static_cast<const float*>(prob), prob_ld, rm, n, d_n,
-                                                                policy, value, act, seed, step, group);
+    const char* hl = getenv("MFX_ACNET_HE_LDS");                    // A/B only: 0 = h_emb held in registers
+    const bool lds = q->dev.Fp <= kHeF && !(hl && atoi(hl) == 0);
+#define MFX_ACNET_LAUNCH(PT, MF, LDS, PB)                                                                              \
+    k_acnet<PT, MF, LDS><<<grid, 256, LDS ? kAcnetLdsSmem : kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld, PB, \
+                                                                            prob_ld, rm, n, d_n, policy, value, act,   \
+                                                                            seed, step, group)
+    const double* pd = static_cast<const double*>(prob);
+    const float* pf = static_cast<const float*>(prob);
+    if (q->dev.use_mf && prob_f64) {
+        if (lds) MFX_ACNET_LAUNCH(double, true, true, pd); else MFX_ACNET_LAUNCH(double, true, false, pd);
+    } else if (q->dev.use_mf) {
+        if (lds) MFX_ACNET_LAUNCH(float, true, true, pf); else MFX_ACNET_LAUNCH(float, true, false, pf);
     } else {
-        k_acnet<float, false><<<grid, 256, kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld, nullptr, 0, rm, n,
-                                                             d_n, policy, value, act, seed, step, group);
+        if (lds) MFX_ACNET_LAUNCH(float, false, true, pf); else MFX_ACNET_LAUNCH(float, false, false, pf);
     }
+#undef MFX_ACNET_LAUNCH
     MFX_HIP(hipGetLastError());
     return 0;
 }

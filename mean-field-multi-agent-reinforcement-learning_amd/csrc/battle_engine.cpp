@@ -1178,6 +1178,10 @@ public:
             }
             ra.renumber = 0;
             ra.lds_step = 0;
+            {
+                const char* qt = getenv("MFX_QUEUE_TIERS");              // A/B only: 0 = consecutive ranks
+                ra.queue_tiers = !(qt && atoi(qt) == 0);
+            }
             if (ro_big) {
                 ro_grid = E;
                 ro_sort.ensure((size_t)E * s.acap);

@@ -9,6 +9,7 @@
 // wave per row with its loads in flight ahead of its stores (scripts/bench_replay.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "mfx_common.h"
 #include "../../include/magent_amd.h"
@@ -114,6 +115,99 @@ __global__ void __launch_bounds__(256) k_rows_copy(RowCols c, const int64_t* __r
     }
 }
 
+// The same move, software-pipelined, for the common shape (MemoryGroup.sample, tight, push: at most one wide
+// column, 4-B aligned, <= 64 x kPipeU dwords per row, and at most 64 narrow units): each wave keeps two rows in
+// flight -- row k + 1's loads are issued before row k's stores, so the in-order vmcnt of gfx9 lets the stores
+// of one row drain under the loads of the next instead of serialising load -> store per row -- and reads its row
+// indices through scalar loads (the row is wave-uniform), which wait on lgkmcnt, not behind the data loads.
+constexpr int kPipeU = 20;
+struct PipeRow {
+    int64_t s, d;
+    bool ok;
+    uint32_t u;                    // this lane's narrow unit (dword, or byte in the low 8 bits)
+    uint32_t v[kPipeU];            // this lane's dwords of the wide column
+};
+
+__global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wdw, const int64_t* __restrict__ idx,
+                                                   int64_t src_mod, int64_t src_rows, int64_t dst_start,
+                                                   int64_t dst_cap, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t W = (int64_t)gridDim.x * 4;
+    const int64_t first = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int units = c.ustart[kRowCols];
+    // this lane's narrow unit: column, byte offset, width (fixed for the whole launch)
+    int uk = -1, uoff = 0, uw = 0;
+    if (lane < units) {
+        uk = 0;
+        while (lane >= c.ustart[uk + 1]) ++uk;
+        uw = c.ubytes[uk];
+        uoff = (lane - c.ustart[uk]) * uw;
+    }
+    auto locate = [&](int64_t i, PipeRow& r) {
+        r.ok = i < n;
+        if (!r.ok) return;
+        int64_t s = idx ? idx[i] : i;                      // wave-uniform: a scalar load
+        const int64_t raw = s;
+        if (src_mod > 0) { s %= src_mod; if (s < 0) s += src_mod; }
+        if (s < 0 || s >= src_rows) {
+            if (lane == 0) atomicCAS(&g_rows_bad, 0ull, (unsigned long long)raw + 1ull);
+            r.ok = false;
+            return;
+        }
+        int64_t d = dst_start + i;
+        if (dst_cap > 0 && d >= dst_cap) d %= dst_cap;
+        r.s = s;
+        r.d = d;
+    };
+    auto fetch = [&](PipeRow& r) {
+        if (!r.ok) return;
+        if (uk >= 0) {
+            const char* sp = c.src[uk] + r.s * c.bytes[uk] + uoff;
+            r.u = uw == 4 ? *reinterpret_cast<const uint32_t*>(sp) : (uint32_t)*reinterpret_cast<const uint8_t*>(sp);
+        }
+        if (wk >= 0) {
+            const uint32_t* sp = reinterpret_cast<const uint32_t*>(c.src[wk] + r.s * c.bytes[wk]);
+#pragma unroll
+            for (int j = 0; j < kPipeU; ++j) {
+                const int64_t q = lane + 64 * j;
+                if (q < wdw) r.v[j] = sp[q];
+            }
+        }
+    };
+    auto put = [&](const PipeRow& r) {
+        if (!r.ok) return;
+        if (uk >= 0) {
+            char* dp = c.dst[uk] + r.d * c.bytes[uk] + uoff;
+            if (uw == 4) *reinterpret_cast<uint32_t*>(dp) = r.u;
+            else *reinterpret_cast<uint8_t*>(dp) = (uint8_t)r.u;
+        }
+        if (wk >= 0) {
+            uint32_t* dp = reinterpret_cast<uint32_t*>(c.dst[wk] + r.d * c.bytes[wk]);
+#pragma unroll
+            for (int j = 0; j < kPipeU; ++j) {
+                const int64_t q = lane + 64 * j;
+                if (q < wdw) dp[q] = r.v[j];
+            }
+        }
+    };
+    PipeRow a, b;
+    int64_t i = first;
+    locate(i, a);
+    fetch(a);
+    while (i < n) {
+        const int64_t i1 = i + W;
+        locate(i1, b);
+        fetch(b);                                          // row i1 in flight ...
+        put(a);                                            // ... while row i drains
+        if (i1 >= n) break;
+        const int64_t i2 = i1 + W;
+        locate(i2, a);
+        fetch(a);
+        put(b);
+        i = i2;
+    }
+}
+
 }  // namespace mfx
 
 using namespace mfx;
@@ -155,7 +249,32 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
         }
     }
     for (int k = n_cols; k <= kRowCols; ++k) c.ustart[k] = units;
+    // the pipelined form takes at most one wide column (4-B aligned, <= 64 x kPipeU dwords) and <= 64 units
+    int wide = -1, n_wide = 0;
+    for (int k = 0; k < n_cols; ++k)
+        if (!c.ubytes[k]) { wide = k; ++n_wide; }
+    const bool pipe = n_wide <= 1 && units <= 64 &&
+                      (wide < 0 || ((((uintptr_t)dst[wide] | (uintptr_t)src[wide] | (uintptr_t)row_bytes[wide]) & 3) == 0 &&
+                                    row_bytes[wide] / 4 <= 64 * kPipeU));
+    const char* pe = getenv("MFX_ROWS_PIPE");              // 0: the one-row-per-wave form (A/B, tests)
+    const int use_pipe = pe ? atoi(pe) : 1;
     const int64_t wgs = (n + 3) / 4;
+    if (pipe && use_pipe) {
+        // persistent-sized grid (what fits at once: 7 waves per SIMD), each wave walking its rows two in flight
+        static const int cus = [] {
+            int dev = 0, n_cu = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+            return n_cu;
+        }();
+        static const int per_cu = [] { const char* e = getenv("MFX_ROWS_WG_PER_CU"); return e ? atoi(e) : 7; }();
+        const int64_t cap = (int64_t)cus * per_cu;
+        const int grid = (int)(wgs < cap ? wgs : cap);
+        k_rows_pipe<<<grid, 256, 0, (hipStream_t)stream>>>(c, wide, wide >= 0 ? row_bytes[wide] / 4 : 0, d_idx,
+                                                           src_mod, src_rows, dst_start, dst_cap, n);
+        MFX_HIP(hipGetLastError());
+        return 0;
+    }
     const int grid = (int)(wgs < 65536 ? wgs : 65536);
     k_rows_copy<<<grid, 256, 0, (hipStream_t)stream>>>(c, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
     MFX_HIP(hipGetLastError());

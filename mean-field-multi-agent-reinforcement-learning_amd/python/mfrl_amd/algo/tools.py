@@ -362,7 +362,7 @@ class Runner:
             models=self.models, print_every=50, eps=variant_eps,
             render=(iteration + 1) % self.render_every if self.render_every > 0 else False, train=self.train)
         if torch.cuda.is_available() and torch.cuda.is_initialized():
-            replay.check()            # once per round: a replay move that met an out-of-range row index raises
+            replay.check_errors()            # once per round: a replay move that met an out-of-range row index raises
         for i, tag in enumerate(["main", "opponent"]):
             info[tag]["total_reward"] = total_rewards[i]
             info[tag]["kill"] = max_nums[i] - nums[1 - i]

@@ -15,7 +15,7 @@ def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
     """For i < n: row (idx[i] if idx is not None else i), taken modulo src_mod if > 0, of every tensor in
     `src` -> row dst_start + i (modulo dst_cap if > 0) of the matching tensor in `dst`.  Tensors: CUDA,
     contiguous, first dimension = rows, equal row byte sizes pairwise.  A source index outside the source
-    rows is skipped on the device and raised by the next check() (the reference's numpy indexing raises
+    rows is skipped on the device and raised by the next check_errors() (the reference's numpy indexing raises
     IndexError at once; checking here would synchronise every move)."""
     assert len(dst) == len(src) and 0 < len(dst) <= _MAX_COLS
     if n is None:
@@ -43,7 +43,7 @@ def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
           "mfx_rows_copy")
 
 
-def check():
+def check_errors():
     """Synchronise the current stream; raise IndexError if a rows_copy since the last check met a source
     index outside its source rows (that row was skipped)."""
     L = lib()

@@ -20,3 +20,7 @@ for E in 8192 131072; do
 MAGENT_LIB=$L timeout -k 10 200 python scripts/timeline_rollout.py --envs $E --substeps 20 > $O/tl_$E.txt 2>&1 || { tail -20 $O/tl_$E.txt; exit 1; }
 cat $O/tl_$E.txt
 done
+for V in "MFX_ROWS_PIPE=0" "MFX_ROWS_PIPE=1 MFX_ROWS_WG_PER_CU=4" "MFX_ROWS_PIPE=1 MFX_ROWS_WG_PER_CU=7" "MFX_ROWS_PIPE=1 MFX_ROWS_WG_PER_CU=14"; do
+  env $V timeout -k 10 200 python scripts/bench_replay.py --cpu-seconds 1 > $O/replay.json 2> $O/err || { tail -20 $O/err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['roofline']['achieved'], d['roofline']['frac'])" $O/replay.json "$V"
+done

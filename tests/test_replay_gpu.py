@@ -16,9 +16,13 @@ def _cols(n, gen):
             torch.rand((n, 21), generator=gen, device="cuda", dtype=torch.float64)]
 
 
+@pytest.mark.parametrize("pipe", ["1", "0"])
 @pytest.mark.parametrize("n_src,n,cap,start,mod", [(1000, 1000, 0, 0, 0), (1000, 700, 2000, 1500, 0),
-                                                   (300, 257, 300, 250, 300), (50, 1, 0, 7, 0)])
-def test_rows_copy_matches_torch_indexing(n_src, n, cap, start, mod):
+                                                   (300, 257, 300, 250, 300), (50, 1, 0, 7, 0), (40000, 33333, 0, 0, 0)])
+def test_rows_copy_matches_torch_indexing(n_src, n, cap, start, mod, pipe, monkeypatch):
+    """pipe 1: the two-rows-in-flight form (k_rows_pipe: one wide column, <= 64 narrow units -- these five columns);
+    0: the one-row-per-wave form (k_rows_copy, which also takes every other column shape)."""
+    monkeypatch.setenv("MFX_ROWS_PIPE", pipe)
     from mfrl_amd.replay import rows_copy
     gen = torch.Generator(device="cuda").manual_seed(n + start)
     src = _cols(n_src, gen)
@@ -43,23 +47,23 @@ def test_rows_copy_matches_torch_indexing(n_src, n, cap, start, mod):
     torch.cuda.synchronize()
     for a, x in zip(dst2, src):
         assert torch.equal(a, x[:n])
-    from mfrl_amd.replay import check
-    check()                                      # no index was out of range
+    from mfrl_amd.replay import check_errors
+    check_errors()                                      # no index was out of range
 
 
 def test_rows_copy_out_of_range_index_raises():
     """An index past the source rows (numpy indexing raises IndexError in the reference's MemoryGroup) skips
-    its row instead of reading out of bounds, and the next check() raises with the first such index; the
+    its row instead of reading out of bounds, and the next check_errors() raises with the first such index; the
     rows with valid indices are still moved and the error word is cleared by the check."""
-    from mfrl_amd.replay import check, rows_copy
+    from mfrl_amd.replay import check_errors, rows_copy
     gen = torch.Generator(device="cuda").manual_seed(3)
     src = _cols(64, gen)
     dst = [torch.zeros((4,) + tuple(x.shape[1:]), dtype=x.dtype, device="cuda") for x in src]
     idx = torch.tensor([5, 64, 7, 1 << 40], dtype=torch.int64, device="cuda")
     rows_copy(dst, src, idx)
     with pytest.raises(IndexError, match="out of range"):
-        check()
-    check()                                      # cleared
+        check_errors()
+    check_errors()                                      # cleared
     for a, x in zip(dst, src):
         assert torch.equal(a[0], x[5]) and torch.equal(a[2], x[7])
         assert not a[1].any() and not a[3].any()
