@@ -1179,8 +1179,10 @@ public:
             ra.renumber = 0;
             ra.lds_step = 0;
             {
-                const char* qt = getenv("MFX_QUEUE_TIERS");              // A/B only: 0 = consecutive ranks
-                ra.queue_tiers = !(qt && atoi(qt) == 0);
+                // A/B only: 0 = the round-3 queue (consecutive ranks, claims two envs ahead), 2 = tiers without the
+                // restart-aware filing weights
+                const char* qt = getenv("MFX_QUEUE_TIERS");
+                ra.queue_tiers = qt ? std::min(std::max(atoi(qt), 0), 2) : 1;
             }
             if (ro_big) {
                 ro_grid = E;

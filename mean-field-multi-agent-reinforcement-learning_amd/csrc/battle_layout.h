@@ -230,9 +230,11 @@ struct RolloutArgs {
     int renumber;                   // large envs: clear_dead renumbers the slots to the list order, so
                                     //   the per-slot arrays of the live agents stay dense (rid keeps ids);
                                     //   2: without the identity fast path (A/B only)
-    int queue_tiers;                // k_rollout: each workgroup's three initial envs come from three tiers of the
-                                    //   heaviest-first order (ranks j, 2G - 1 - j, 2G + j of G workgroups), not
-                                    //   three consecutive ranks -- 0: consecutive (A/B only)
+    int queue_tiers;                // k_rollout: each workgroup's two initial envs come from two tiers of the
+                                    //   heaviest-first order (ranks b, 2G - 1 - b of G workgroups), it claims one
+                                    //   env ahead instead of two, and files envs by their weight over the next
+                                    //   launch (a cap restart inside it counts) -- 0: round 3 (A/B only), 2: tiers
+                                    //   without the restart-aware weights (A/B only)
     int lds_step;                   // few LDS-sized envs on the queue kernel: big_env_step stages the env in
                                     //   LDS for the step and writes it back (BigLayout::img)
     float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and

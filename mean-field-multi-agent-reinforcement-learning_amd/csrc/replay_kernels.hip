@@ -208,6 +208,82 @@ __global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wd
     }
 }
 
+// A/B form (MFX_ROWS_PIPE=2/3): R rows per wave loaded together, then stored together (R x ~4.7 KB in flight per
+// wave instead of two rows staggered); kNt: the destination rows written with nontemporal stores.
+template <int R, bool kNt>
+__global__ void __launch_bounds__(256) k_rows_batch(RowCols c, int wk, int64_t wdw, const int64_t* __restrict__ idx,
+                                                    int64_t src_mod, int64_t src_rows, int64_t dst_start,
+                                                    int64_t dst_cap, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t W = (int64_t)gridDim.x * 4;
+    const int64_t first = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int units = c.ustart[kRowCols];
+    int uk = -1, uoff = 0, uw = 0;
+    if (lane < units) {
+        uk = 0;
+        while (lane >= c.ustart[uk + 1]) ++uk;
+        uw = c.ubytes[uk];
+        uoff = (lane - c.ustart[uk]) * uw;
+    }
+    for (int64_t i0 = first; i0 < n; i0 += (int64_t)R * W) {
+        PipeRow r[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t i = i0 + k * W;
+            r[k].ok = i < n;
+            if (!r[k].ok) continue;
+            int64_t sidx = idx ? idx[i] : i;
+            const int64_t raw = sidx;
+            if (src_mod > 0) { sidx %= src_mod; if (sidx < 0) sidx += src_mod; }
+            if (sidx < 0 || sidx >= src_rows) {
+                if (lane == 0) atomicCAS(&g_rows_bad, 0ull, (unsigned long long)raw + 1ull);
+                r[k].ok = false;
+                continue;
+            }
+            int64_t d = dst_start + i;
+            if (dst_cap > 0 && d >= dst_cap) d %= dst_cap;
+            r[k].s = sidx;
+            r[k].d = d;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (!r[k].ok) continue;
+            if (uk >= 0) {
+                const char* sp = c.src[uk] + r[k].s * c.bytes[uk] + uoff;
+                r[k].u = uw == 4 ? *reinterpret_cast<const uint32_t*>(sp) : (uint32_t)*reinterpret_cast<const uint8_t*>(sp);
+            }
+            if (wk >= 0) {
+                const uint32_t* sp = reinterpret_cast<const uint32_t*>(c.src[wk] + r[k].s * c.bytes[wk]);
+#pragma unroll
+                for (int j = 0; j < kPipeU; ++j) {
+                    const int64_t q = lane + 64 * j;
+                    if (q < wdw) r[k].v[j] = sp[q];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (!r[k].ok) continue;
+            if (uk >= 0) {
+                char* dp = c.dst[uk] + r[k].d * c.bytes[uk] + uoff;
+                if (uw == 4) *reinterpret_cast<uint32_t*>(dp) = r[k].u;
+                else *reinterpret_cast<uint8_t*>(dp) = (uint8_t)r[k].u;
+            }
+            if (wk >= 0) {
+                uint32_t* dp = reinterpret_cast<uint32_t*>(c.dst[wk] + r[k].d * c.bytes[wk]);
+#pragma unroll
+                for (int j = 0; j < kPipeU; ++j) {
+                    const int64_t q = lane + 64 * j;
+                    if (q < wdw) {
+                        if (kNt) __builtin_nontemporal_store(r[k].v[j], dp + q);
+                        else dp[q] = r[k].v[j];
+                    }
+                }
+            }
+        }
+    }
+}
+
 }  // namespace mfx
 
 using namespace mfx;
@@ -260,18 +336,27 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
     const int use_pipe = pe ? atoi(pe) : 1;
     const int64_t wgs = (n + 3) / 4;
     if (pipe && use_pipe) {
-        // persistent-sized grid (what fits at once: 7 waves per SIMD), each wave walking its rows two in flight
+        // persistent-sized grid, each wave walking its rows two in flight
         static const int cus = [] {
             int dev = 0, n_cu = 0;
             if (hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
             return n_cu;
         }();
-        static const int per_cu = [] { const char* e = getenv("MFX_ROWS_WG_PER_CU"); return e ? atoi(e) : 7; }();
+        // 4 workgroups per CU: 0.555-0.559 of the HBM peak on the MF-Q sample against 0.464 / 0.520 at 7 / 14 and
+        // 0.510-0.537 for the one-row-per-wave form (profiles/r04_replay_ab.txt)
+        static const int per_cu = [] { const char* e = getenv("MFX_ROWS_WG_PER_CU"); return e ? atoi(e) : 4; }();
         const int64_t cap = (int64_t)cus * per_cu;
         const int grid = (int)(wgs < cap ? wgs : cap);
-        k_rows_pipe<<<grid, 256, 0, (hipStream_t)stream>>>(c, wide, wide >= 0 ? row_bytes[wide] / 4 : 0, d_idx,
-                                                           src_mod, src_rows, dst_start, dst_cap, n);
+        const int64_t wdw = wide >= 0 ? row_bytes[wide] / 4 : 0;
+        const char* ne = getenv("MFX_ROWS_NT");
+        const bool nt = ne && atoi(ne) == 1;
+        hipStream_t st = (hipStream_t)stream;
+        if (use_pipe == 2 && nt) k_rows_batch<4, true><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
+        else if (use_pipe == 2) k_rows_batch<4, false><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
+        else if (use_pipe == 3 && nt) k_rows_batch<2, true><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
+        else if (use_pipe == 3) k_rows_batch<2, false><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
+        else k_rows_pipe<<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
         MFX_HIP(hipGetLastError());
         return 0;
     }

@@ -19,3 +19,8 @@ done; done
 L=mean-field-multi-agent-reinforcement-learning_amd/build/libmagent_stamps.so
 MFX_QUEUE_TIERS=1 MAGENT_LIB=$L timeout -k 10 200 python scripts/timeline_rollout.py --envs 8192 --substeps 20 > $O/tl_8192_t1.txt 2>&1 || { tail -20 $O/tl_8192_t1.txt; exit 1; }
 cat $O/tl_8192_t1.txt
+for rep in 1 2; do
+for V in "MFX_ROWS_PIPE=0" "MFX_ROWS_PIPE=1 MFX_ROWS_WG_PER_CU=4" "MFX_ROWS_PIPE=2 MFX_ROWS_WG_PER_CU=4" "MFX_ROWS_PIPE=2 MFX_ROWS_WG_PER_CU=8" "MFX_ROWS_PIPE=2 MFX_ROWS_NT=1 MFX_ROWS_WG_PER_CU=4" "MFX_ROWS_PIPE=3 MFX_ROWS_WG_PER_CU=6" "MFX_ROWS_PIPE=3 MFX_ROWS_NT=1 MFX_ROWS_WG_PER_CU=6"; do
+  env $V timeout -k 10 200 python scripts/bench_replay.py --cpu-seconds 1 > $O/replay.json 2> $O/err || { tail -20 $O/err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], '%.4e' % d['value'], '%.1f' % d['roofline']['achieved'], '%.4f' % d['roofline']['frac'])" $O/replay.json "$V"
+done; done
