@@ -111,6 +111,21 @@ def rank_device(world, local, device_count, backend):
     return local % device_count, min(world, device_count)
 
 
+class _StdoutToStderr:
+    """fd 1 -> fd 2 while the process group initialises: the gloo library prints its connection messages on
+    stdout from C++, and the bench's stdout must carry exactly one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def rank_envs(args, world, rank):
     """Envs this rank steps: --envs per rank, or its share of --total-envs (remainder to low ranks)."""
     if args.total_envs is None:
@@ -166,7 +181,8 @@ def launcher_selftest(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")
+        with _StdoutToStderr():
+            dist.init_process_group("gloo")
     if world > 1 and args.fail_rank >= 0:
         # a rank that dies while the others wait in a collective: rank fail_rank exits 3 once every other
         # rank has announced (through the rendezvous store) that it is entering the barrier
@@ -425,7 +441,8 @@ def main():
         if args.backend == "nccl":           # RCCL over xGMI
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:                                # rehearsal of the N-rank flow without RCCL
-            dist.init_process_group(args.backend)
+            with _StdoutToStderr():
+                dist.init_process_group(args.backend)
     E = rank_envs(args, world, rank)
     stream = torch.cuda.current_stream()
     left, right = bd.block_positions(args.map, args.agents // 2)
