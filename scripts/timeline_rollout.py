@@ -58,6 +58,17 @@ for L in range(a.launches):
         if sel.any():
             print("  agents %4d-%-4s: %5d units, duration mean %7.1f us, max %7.1f us, started by %6.3f ms"
                   % (lo, hi if hi < 10 ** 9 else "", sel.sum(), dur[sel].mean(), dur[sel].max(), t0[sel].max() / 1e3))
+    n_last = st[:, 16]                                          # agents at the launch's last step of the env
+    light = n0 <= 63
+    rst = light & (n_last > 128)                                # restarted inside the launch (256 placed again)
+    print("  light units (<= 63 agents at install) that restarted inside the launch: %d of %d, duration mean %.1f us, "
+          "max %.1f us; light units without a restart: mean %.1f us, max %.1f us"
+          % (rst.sum(), light.sum(), dur[rst].mean() if rst.any() else 0.0, dur[rst].max() if rst.any() else 0.0,
+             dur[light & ~rst].mean(), dur[light & ~rst].max()))
+    slow = light & ~rst & (dur > 2000)
+    if slow.any():
+        print("  slow light units without a restart: %d, agents at install %s, finished at %s ms, workgroups %s"
+              % (slow.sum(), n0[slow][:12].tolist(), np.round(t1[slow][:12] / 1e3, 2).tolist(), wg[slow][:12].tolist()))
     busy = np.bincount(wg, weights=dur, minlength=grid)
     last = np.zeros(grid)
     np.maximum.at(last, wg, t1)
