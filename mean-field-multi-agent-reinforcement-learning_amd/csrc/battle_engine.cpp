@@ -221,6 +221,8 @@ public:
     bool ro_bigq = false;
     bool ro_bigq_want = true;                // MFX_BIG_FUSED=0 at rollout_init: the two-stream pipeline (A/B)
     DevBuf<uint32_t> ro_q_items, ro_q_si;    // [2][kXcds][list cap] tagged items; [E] next step index
+    DevBuf<uint8_t> ro_snap;                 // few_pipe: [E][2] observation snapshots
+    DevBuf<int32_t> ro_q_step;               // few_pipe: [kXcds] stepper claims
     DevBuf<int32_t> ro_q_cnt, ro_q_left, ro_q_done;
     int ro_q_grid = 0, ro_qpar = 0;
     uint32_t ro_qlaunch = 0, ro_qdone = 0;   // launches so far (item tags); env-steps the queue has done
@@ -1235,6 +1237,17 @@ public:
                         ra.q_items = ro_q_items.p; ra.q_cnt = ro_q_cnt.p; ra.q_left = ro_q_left.p;
                         ra.q_si = ro_q_si.p; ra.q_done = ro_q_done.p; ra.q_list_cap = lcap;
                         ra.obs_item_rows = Rq;
+                        // few envs with the env staged in LDS: the pipelined form (a stepper workgroup per env
+                        // steps while the items observe its snapshot) while the steppers leave at least 3 of 4
+                        // of every XCD's workgroups to the items
+                        const char* fp = getenv("MFX_FEW_PIPE");                // A/B only: 0 = off
+                        ra.few_pipe = ra.lds_step && E <= ro_q_grid / 4 && !(fp && atoi(fp) == 0);
+                        if (ra.few_pipe) {
+                            ra.few_snap_bytes = few_snap_bytes(s.cells_n, s.cap, n_groups());
+                            ro_snap.ensure((size_t)E * 2 * ra.few_snap_bytes);
+                            ro_q_step.ensure(kXcds);
+                            ra.few_snap = ro_snap.p; ra.q_step = ro_q_step.p;
+                        }
                         const char* qg = getenv("MFX_BIGQ_GRID");               // sweeps only
                         // (a multiple of kXcds: every XCD's list needs workgroups of its own)
                         if (qg && atoi(qg) > 0)
@@ -1297,6 +1310,34 @@ public:
         {
             const State& planned = ro_pipe ? ro_pipe_host[ro_par].s : ro_ctx_host.s;
             if (s.cap != ro_cap || memcmp(&planned, &s, sizeof(State)) != 0) MFX_CHECK(rollout_plan());
+        }
+        if (ro_big && ro_bigq && ra.few_pipe) {
+            // the pipelined few-env form: every launch files and observes its own items (parity 0, a fresh tag),
+            // the steppers claimed per XCD; q_left must read 0 (no items outstanding) at a launch start
+            MFX_CHECK(sync_cells());
+            const size_t lst = (size_t)kXcds * kObsCntPad;
+            if (ro_prep_stale) {
+                ro_qdone = 0;
+                ro_qlaunch++;
+                MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
+                MFX_HIP(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
+                MFX_HIP(hipMemsetAsync(ro_q_left.p, 0, (size_t)E * sizeof(int32_t), stream));
+            }
+            ro_prep_stale = false;
+            for (int i = 0; i < n_steps;) {
+                const int k = std::min(ro_sub, n_steps - i);
+                MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, lst * sizeof(int32_t), stream));
+                MFX_HIP(hipMemsetAsync(ro_q_step.p, 0, kXcds * sizeof(int32_t), stream));
+                ro_qdone += (uint32_t)E * (uint32_t)k;
+                MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, 0,
+                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
+                                            ra.lds_step, stream, true));
+                ro_qlaunch++;
+                ro_launch++;
+                ra.step_index += k;
+                i += k;
+            }
+            return 0;
         }
         if (ro_big && ro_bigq) {
             MFX_CHECK(sync_cells());

@@ -314,7 +314,7 @@ hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, bool lds
     hipError_t err = hipGetDevice(&dev);
     if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (err == hipSuccess)
-        err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rollout_bigq, kBigRolloutThreads, smem);
+        err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rollout_bigq<false>, kBigRolloutThreads, smem);
     if (err != hipSuccess) return err;
     // one device of all 8 XCDs (SPX, 32 CUs each): every XCD gets workgroups of the full-occupancy grid,
     // and the XCC ids are 0-7 (k_rollout_bigq keeps each env on XCD e % 8)
@@ -330,13 +330,19 @@ hipError_t launch_bigq_seed(const GameParams* d_gp, const State& s, const Rollou
 
 hipError_t launch_rollout_bigq(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                                int rows, uint32_t si0, int n_sub, int par, uint32_t tag_cur, uint32_t tag_next,
-                               int32_t done_target, int grid, bool lds_env, hipStream_t st) {
+                               int32_t done_target, int grid, bool lds_env, hipStream_t st, bool pipe) {
     const size_t smem = bigq_smem_bytes(gp, s.cap, s.acap, rows, lds_env);
-    if (smem > 160 * 1024 || grid < 1 || n_sub < 1) return hipErrorInvalidValue;
-    k_rollout_bigq<<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
-                                                          done_target);
+    if (smem > 160 * 1024 || grid < 1 || n_sub < 1 || (pipe && !lds_env)) return hipErrorInvalidValue;
+    if (pipe)
+        k_rollout_bigq<true><<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
+                                                                    done_target);
+    else
+        k_rollout_bigq<false><<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
+                                                                     done_target);
     return hipGetLastError();
 }
+
+size_t few_snap_bytes(int cells_n, int cap, int G) { return snap_layout(cells_n, cap, G).total; }
 
 hipError_t launch_clear_dead(const GameParams* d_gp, const State& s, hipStream_t st) {
     k_clear_dead<<<s.E, 256, 0, st>>>(d_gp, s);

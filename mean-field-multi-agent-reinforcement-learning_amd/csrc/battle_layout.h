@@ -256,6 +256,13 @@ struct RolloutArgs {
     uint32_t* q_si;                 //   [E] the env's next step index
     int32_t* q_done;                //   [kObsCntPad] 0: env-steps done (monotone), 2: stuck-queue error word
     size_t q_list_cap;              //   items per list and parity
+    int few_pipe;                   // few LDS-sized envs on the queue kernel, pipelined: one stepper workgroup
+                                    //   per env keeps it in LDS for the whole launch and steps it while the
+                                    //   item workers observe the state the step started from, out of a
+                                    //   per-env snapshot (few_snap, 2 parities) -- k_rollout_bigq<true>
+    uint8_t* few_snap;              //   [E][2][few_snap_bytes] (snap_layout)
+    size_t few_snap_bytes;
+    int32_t* q_step;                //   [kXcds] stepper roles claimed per XCD this launch (zeroed per launch)
     const uint4* wall_image;        // [H*W] u16 cells of that image with the agents removed: every
                                     // install rebuilds the cells from it plus the agents' positions, so
                                     // per-env cells are neither read nor written back (State::cells is

@@ -957,3 +957,29 @@ def test_rollout_lds_step_matches_hbm_step(monkeypatch):
         del eng
     for (k, x), (_, y) in zip(dumps[0], dumps[1]):
         assert torch.equal(x, y), k
+
+
+@pytest.mark.parametrize("E,S", [(8, 20), (64, 7), (100, 1)])
+def test_rollout_few_pipe_matches_queue_step(E, S, monkeypatch):
+    """The pipelined few-env form (RolloutArgs::few_pipe, the default for <= grid / 4 LDS-sized envs: a stepper
+    workgroup per env keeps it in LDS and steps while the items observe its snapshot) against the queue kernel's
+    step-after-items form (MFX_FEW_PIPE=0): staggered 64x64 envs, 432 steps (every env restarts), every output
+    buffer and the per-call ids / positions / hp bit for bit -- E not a multiple of the 8 XCDs, 1 and 7 steps per
+    launch included."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    N, T = 128, 432
+    left, right = bd.block_positions(64, N)
+    dumps = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MFX_FEW_PIPE", mode)
+        eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=4321, stagger=True)
+        eng.rollout_substeps(S)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        eng.rollout_step(T)
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, N))
+        del eng
+    for (k, x), (_, y) in zip(dumps[0], dumps[1]):
+        assert torch.equal(x, y), k
