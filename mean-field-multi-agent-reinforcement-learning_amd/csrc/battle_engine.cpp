@@ -258,6 +258,8 @@ public:
     // (4.0e8 vs 3.2e8).  16-agent items: 0.0435 ms per step at 8 envs vs 0.0461 (32), 0.0497 (64), 0.0441 (8).
     static constexpr int kSmallEMax = 1024;
     static constexpr int kSmallERows = 16;
+    // the pipelined few-env stepper: wave 0 alone steps envs of up to this many agents (k_rollout's threshold)
+    static constexpr int kFewWaveMax = 64;
     static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
     hipStream_t ro_str[kMaxSplit] = {};
@@ -1180,6 +1182,7 @@ public:
             }
             ra.renumber = 0;
             ra.lds_step = 0;
+            ra.few_pipe = 0;
             {
                 // A/B only: 0 = the round-3 queue (consecutive ranks, claims two envs ahead), 2 = tiers without the
                 // restart-aware filing weights
@@ -1243,6 +1246,8 @@ public:
                         const char* fp = getenv("MFX_FEW_PIPE");                // A/B only: 0 = off
                         ra.few_pipe = ra.lds_step && E <= ro_q_grid / 4 && !(fp && atoi(fp) == 0);
                         if (ra.few_pipe) {
+                            const char* fw = getenv("MFX_FEW_WAVE_MAX");        // A/B only
+                            ra.few_wave_max = fw ? std::max(0, atoi(fw)) : kFewWaveMax;
                             ra.few_snap_bytes = few_snap_bytes(s.cells_n, s.cap, n_groups());
                             ro_snap.ensure((size_t)E * 2 * ra.few_snap_bytes);
                             ro_q_step.ensure(kXcds);
@@ -1490,9 +1495,11 @@ public:
 
     // Lanes over which the rollout sums a group's rewards of an env with n agents (the order the episode
     // returns follow): k_rollout's wave 0 up to 64 agents, else its workgroup; the step of the large-env
-    // and few-env paths (big_env_step) 512 lanes.
+    // and few-env queue paths (big_env_step) 512 lanes; the pipelined few-env stepper (few_env_step) k_rollout's
+    // team forms: wave 0 up to 64 agents, else its 512-lane workgroup.
     int rollout_sum_lanes(int n) const {
         if (!rollout_ready) return -1;
+        if (ro_big && ro_bigq && ra.few_pipe) return n <= ra.few_wave_max ? 64 : 512;
         if (ro_big) return 512;                       // kBigRolloutThreads (battle/rollout_big.inc)
         return n <= 64 ? 64 : 256;
     }

@@ -257,6 +257,7 @@ struct RolloutArgs {
     int32_t* q_done;                //   [kObsCntPad] 0: env-steps done (monotone), 2: stuck-queue error word
     size_t q_list_cap;              //   items per list and parity
     int few_pipe;                   // few LDS-sized envs on the queue kernel, pipelined: one stepper workgroup
+    int few_wave_max;               // few_pipe: the stepper's wave team (wave 0 alone) up to this many agents, else the workgroup
                                     //   per env keeps it in LDS for the whole launch and steps it while the
                                     //   item workers observe the state the step started from, out of a
                                     //   per-env snapshot (few_snap, 2 parities) -- k_rollout_bigq<true>
