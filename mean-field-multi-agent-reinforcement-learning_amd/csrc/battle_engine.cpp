@@ -1251,8 +1251,6 @@ public:
                             ra.few_wave_max = fw ? std::min(std::max(0, atoi(fw)), kFewWaveMax) : kFewWaveMax;
                             const char* fo = getenv("MFX_FEW_OVERLAP");         // A/B only: 0 = file, then step
                             ra.few_overlap = !(fo && atoi(fo) == 0);
-                            const char* fb = getenv("MFX_FEW_PAR_FORMS");       // A/B only
-                            ra.few_par_forms = fb ? atoi(fb) != 0 : 0;
                             ra.few_snap_bytes = few_snap_bytes(s.cells_n, s.cap, n_groups());
                             ro_snap.ensure((size_t)E * 2 * ra.few_snap_bytes);
                             ro_q_step.ensure(kXcds);

@@ -259,7 +259,6 @@ struct RolloutArgs {
     int few_pipe;                   // few LDS-sized envs on the queue kernel, pipelined: one stepper workgroup
     int few_wave_max;               // few_pipe: the stepper's wave team (wave 0 alone) up to this many agents, else the workgroup
     int few_overlap;                // few_pipe: wave 0 steps while the other waves drain the snapshot and file its items
-    int few_par_forms;              // few_pipe, workgroup team: attack_parallel / move_parallel instead of attack_big / move_jump
                                     //   per env keeps it in LDS for the whole launch and steps it while the
                                     //   item workers observe the state the step started from, out of a
                                     //   per-env snapshot (few_snap, 2 parities) -- k_rollout_bigq<true>
