@@ -8,7 +8,7 @@ the warmup, so any K-step window sees the steady mix of episode phases (not just
 every env of the batch: get_observation for both groups (views + features written to HBM),
 the synthetic rush policy of SURVEY.md 8(d) (on device), set_action, step (attack shuffle,
 attacks, starve, moves, reward rules, done), get_reward, mean-action pooling, clear_dead,
-and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default 20) such
+and episode restart at done / 400 steps.  One k_rollout launch runs --substeps (default: the engine's choice, 20 here) such
 steps of every env back to back while the env's image stays in LDS, for 131072 envs per GPU; the timed
 region is exactly K steps (ceil(K / substeps) launches, the last one the remainder), bit-identical to K
 one-step launches.
@@ -64,9 +64,12 @@ def parse(argv=None):
     # (profiles/r03_substeps20.txt).  The queue kernel k_rollout_bigq (256x256 envs, and batches of few
     # 64x64 envs): 20 steps per launch, +0.3 % over 16 at 60 steps, +1-2 % at 20 steps (one launch, not
     # 16 + 4).  The results are bit-identical for any value
-    # (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps); the engine takes 1..64.
-    ap.add_argument("--substeps", type=int, default=20,
-                    help="consecutive steps of every env per launch (default 20)")
+    # (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps); the engine takes 1..64, and 0 lets it
+    # choose per path and batch (BattleEngine::sub_steps, profiles/r04_substeps_auto.txt): 20 here at 131072 envs
+    # and at 256x256, 2 for k_rollout below 96 envs per CU (8192 envs: 0.556 -> 0.594), 64 for the pipelined
+    # few-env stepper (8 envs: 0.0356 -> 0.0285 ms per step).
+    ap.add_argument("--substeps", type=int, default=0,
+                    help="consecutive steps of every env per launch (default 0: the engine's choice, 20 at the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -451,9 +454,8 @@ def main():
     eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
     path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
     grid, lds = eng.rollout_info()          # persistent grid, LDS bytes per workgroup
-    S = max(1, args.substeps)
-    if S != 1:
-        eng.rollout_substeps(S)
+    eng.rollout_substeps(max(0, args.substeps))
+    S = eng.get_substeps()                  # (0: the engine's choice for this path and batch)
     big = path in ("k_rollout_bigq", "k_observe_items+k_rollout_big")   # large envs, state in HBM
     steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
     stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")

@@ -243,7 +243,7 @@ public:
     int ro_grid = 0, ro_cap = 0;
     // fused rollout: consecutive steps of each env per k_rollout launch (env image kept in LDS between
     // them; the launch's ramp-up / tail and the install / write-back are paid once per ro_sub steps)
-    int ro_sub = 1;
+    int ro_sub = 1;                          // 0: chosen per path and batch (sub_steps)
     // large-env path: the envs split into ro_split independent sub-batches, each a pipeline
     // (k_observe_items -> k_rollout_big) on its own stream, so one sub-batch's latency-bound step
     // overlaps the other's HBM-bound observation.  Each item launch takes a third of the chip's
@@ -1333,7 +1333,7 @@ public:
             }
             ro_prep_stale = false;
             for (int i = 0; i < n_steps;) {
-                const int k = std::min(ro_sub, n_steps - i);
+                const int k = std::min(sub_steps(), n_steps - i);
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, lst * sizeof(int32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_step.p, 0, kXcds * sizeof(int32_t), stream));
                 ro_qdone += (uint32_t)E * (uint32_t)k;
@@ -1366,7 +1366,7 @@ public:
             }
             ro_prep_stale = false;
             for (int i = 0; i < n_steps;) {
-                const int k = std::min(ro_sub, n_steps - i);
+                const int k = std::min(sub_steps(), n_steps - i);
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p + (ro_qpar ^ 1) * lst, 0, lst * sizeof(int32_t), stream));
                 ro_qdone += (uint32_t)E * (uint32_t)k;
                 MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, ro_qpar,
@@ -1436,7 +1436,7 @@ public:
             return 0;
         }
         for (int i = 0; i < n_steps;) {
-            const int k = std::min(ro_sub, n_steps - i);
+            const int k = std::min(sub_steps(), n_steps - i);
             MFX_HIP(launch_rollout(gp, d_gp, s, ro_ctx.p, ra.rowcap, ra.step_index, ra.work_sel, (int)(ro_launch % 6),
                                    ro_grid, 0, k, stream));
             ro_launch++;
@@ -1494,6 +1494,22 @@ public:
         if (!rollout_ready) return -1;
         if (ro_big) return ro_bigq ? 3 : 2;
         return ro_pipe ? 1 : 0;
+    }
+
+    // Steps per launch: ro_sub, or with ro_sub 0 (mfx_battle_rollout_set_substeps(game, 0)) the measured best of the
+    // path (profiles/r04_substeps_auto.txt, one MI355X): the pipelined few-env stepper 64 (the launch ends with
+    // its slowest env's steps, and a longer launch averages each env's heavy early-episode steps with its light
+    // ones: 8 envs 0.0356 -> 0.0285 ms per step from 20 to 64); k_rollout below 96 envs per CU 2 (its workgroups'
+    // heaviest units end the launch: 8192 envs 0.556 -> 0.594 of peak, 16384 0.62 -> 0.63), else 20 (32768
+    // envs 0.75 at 5, 0.77 at 20; the bench's 131072, 0.84-0.86); the large-env queue kernel 20.
+    int sub_steps() const {
+        if (ro_sub > 0) return ro_sub;
+        if (ro_big) return (ro_bigq && ra.few_pipe) ? 64 : 20;
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return E < 96 * cus ? 2 : 20;
     }
 
     // Lanes over which the rollout sums a group's rewards of an env with n agents (the order the episode
@@ -2405,10 +2421,17 @@ MFX_API int mfx_battle_rollout_sum_lanes(void* game, int n_agents, int* lanes) {
 // in LDS; the large-env queue kernel k_rollout_bigq runs that many steps of every env per launch (its
 // item lists hold one filing per env and step of a launch: lcap in rollout_plan, hence <= 64).
 // rollout_step(n) results are identical for any value (the last step's buffers, the same state); only
-// the launch count changes.  Ignored by the two pipelines (one step per launch).
+// the launch count changes.  Ignored by the two pipelines (one step per launch).  0: chosen per path and batch
+// (BattleEnv::sub_steps); mfx_battle_rollout_get_substeps reports the value in force.
 MFX_API int mfx_battle_rollout_set_substeps(void* game, int n_sub) {
-    if (n_sub < 1 || n_sub > 64) return mfx::fail("rollout_set_substeps: %d not in 1..64", n_sub);
+    if (n_sub < 0 || n_sub > 64) return mfx::fail("rollout_set_substeps: %d not in 0..64", n_sub);
     MFX_ENV(game)->ro_sub = n_sub;
+    return 0;
+}
+
+MFX_API int mfx_battle_rollout_get_substeps(void* game, int* n_sub) {
+    if (!MFX_ENV(game)->rollout_ready) return mfx::fail("rollout_get_substeps before rollout_init");
+    *n_sub = MFX_ENV(game)->sub_steps();
     return 0;
 }
 

@@ -33,7 +33,8 @@ class BattleBatch:
                    "mfx_battle_rollout_buffer", "mfx_battle_rollout_copy", "mfx_battle_rollout_rowcap",
                    "mfx_battle_rollout_info", "mfx_battle_group_capacity", "mfx_battle_rollout_set_substeps",
                    "mfx_battle_rollout_copy_at", "mfx_battle_rollout_check", "mfx_battle_rollout_path",
-                   "mfx_battle_rollout_policy_step", "mfx_battle_rollout_sum_lanes", "mfx_battle_rollout_mean_stride"):
+                   "mfx_battle_rollout_policy_step", "mfx_battle_rollout_sum_lanes", "mfx_battle_rollout_mean_stride",
+                   "mfx_battle_rollout_get_substeps"):
             try:
                 getattr(self._dll, fn).restype = ctypes.c_int
             except AttributeError:          # an older build of the library (A/B runs)
@@ -143,8 +144,15 @@ class BattleBatch:
         return p.value
 
     def rollout_substeps(self, n_sub):
-        """Consecutive steps of every env per k_rollout launch (results do not depend on it)."""
+        """Consecutive steps of every env per k_rollout launch (results do not depend on it); 0: the engine
+        picks per path and batch size (get_substeps reports it)."""
         self._check(self._dll.mfx_battle_rollout_set_substeps(self.game, int(n_sub)), "rollout_set_substeps")
+
+    def get_substeps(self):
+        """Steps per launch in force (after rollout_init)."""
+        p = ctypes.c_int()
+        self._check(self._dll.mfx_battle_rollout_get_substeps(self.game, ctypes.byref(p)), "rollout_get_substeps")
+        return p.value
 
     def rollout_step(self, n_steps=1):
         self._check(self._dll.mfx_battle_rollout_step(self.game, n_steps), "rollout_step")

@@ -959,7 +959,7 @@ def test_rollout_lds_step_matches_hbm_step(monkeypatch):
         assert torch.equal(x, y), k
 
 
-@pytest.mark.parametrize("E,S", [(8, 20), (64, 7), (100, 1)])
+@pytest.mark.parametrize("E,S", [(8, 20), (8, 64), (64, 7), (100, 1)])
 def test_rollout_few_pipe_matches_queue_step(E, S, monkeypatch):
     """The pipelined few-env form (RolloutArgs::few_pipe, the default for <= grid / 4 LDS-sized envs: a stepper
     workgroup per env keeps it in LDS and steps while the items observe its snapshot) against the queue kernel's
@@ -983,3 +983,26 @@ def test_rollout_few_pipe_matches_queue_step(E, S, monkeypatch):
         del eng
     for (k, x), (_, y) in zip(dumps[0], dumps[1]):
         assert torch.equal(x, y), k
+
+
+def test_rollout_substeps_auto_choice():
+    """rollout_substeps(0): the engine picks the steps per launch for its path and batch (BattleEngine::sub_steps):
+    64 for the pipelined few-env stepper, 2 for k_rollout below 96 envs per CU, 20 for the large-env queue kernel;
+    an explicit value is reported as given.  The results do not depend on it (test_rollout_substeps_match_single_steps
+    and the few-env replays at 20 and 64 steps per launch)."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    cases = ((64, 256, 8, "k_rollout_bigq", 64), (64, 256, 2048, "k_rollout", 2), (256, 4096, 16, "k_rollout_bigq", 20))
+    for map_size, agents, E, path, want in cases:
+        left, right = bd.block_positions(map_size, agents // 2)
+        eng = BattleBatch(map_size, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=5)
+        assert eng.rollout_path() == path, (E, eng.rollout_path())
+        eng.rollout_substeps(0)
+        assert eng.get_substeps() == want, (map_size, E, eng.get_substeps())
+        eng.rollout_substeps(7)
+        assert eng.get_substeps() == 7
+        eng.rollout_substeps(0)
+        eng.rollout_step(3)
+        eng.rollout_check()
+        del eng
