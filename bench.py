@@ -66,8 +66,8 @@ def parse(argv=None):
     # 16 + 4).  The results are bit-identical for any value
     # (tests/test_rollout_gpu.py::test_rollout_substeps_match_single_steps); the engine takes 1..64, and 0 lets it
     # choose per path and batch (BattleEngine::sub_steps, profiles/r04_substeps_auto.txt): 20 here at 131072 envs
-    # and at 256x256, 2 for k_rollout below 96 envs per CU (8192 envs: 0.556 -> 0.594), 64 for the pipelined
-    # few-env stepper (8 envs: 0.0356 -> 0.0285 ms per step).
+    # and at 256x256, 2 for k_rollout below 96 envs per CU (8192 envs: 0.556 -> 0.594), and for the pipelined
+    # few-env stepper the whole timed region as one launch (8 envs: 0.0356 ms per step at 20, 0.0285 at 64).
     ap.add_argument("--substeps", type=int, default=0,
                     help="consecutive steps of every env per launch (default 0: the engine's choice, 20 at the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -510,7 +510,10 @@ def main():
     check = run_check(eng, args, E, [left, right], env_seed(1234, rank), world)
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
-        units_per_launch = local_units / args.steps * S
+        # agent-steps of one launch the kernel_ms average covers (full-size launches, else all of them)
+        steps_per_timed_launch = S if any(n == S for n in chunks) else args.steps / len(chunks)
+        S_run = max(chunks)                  # the launches of the timed region (S caps them at K steps)
+        units_per_launch = local_units / args.steps * steps_per_timed_launch
         achieved = BYTES_PER_AGENT_STEP * units_per_launch / (kernel_ms * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_big256.json" if big else "pmc_k_rollout.json")
@@ -536,9 +539,9 @@ def main():
                        % (args.map, args.map, args.agents // 2, args.agents // 2,
                           ("%d envs over %d GPUs" % (args.total_envs, world)) if strong else "%d envs per GPU" % E,
                           args.max_steps,
-                          ("%s, %d steps per launch" % (path, S)) if big else
-                          ("fused step" if S == 1 else "fused step, %d consecutive steps per launch" % S)),
-                       "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S,
+                          ("%s, %d steps per launch" % (path, S_run)) if big else
+                          ("fused step" if S_run == 1 else "fused step, %d consecutive steps per launch" % S_run)),
+                       "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S_run,
                        # agents placed per episode start vs the live agents an env-step actually carries (the
                        # unit counts live agents; battles thin the armies, staggered episodes mix all phases)
                        "live_agents_per_env_step": local_units / (args.steps * E),
@@ -547,8 +550,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kernel_ms,
-                         "kernel_ms_is": "mean launch duration (HIP events on the launch stream), %d step(s) per launch"
-                                         % S,
+                         "kernel_ms_is": "mean launch duration (HIP events on the launch stream), %g step(s) per launch"
+                                         % steps_per_timed_launch,
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch,
                          "grid": grid, "lds_bytes": lds},
             "cpu_baseline": None,

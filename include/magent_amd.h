@@ -111,7 +111,8 @@ int mfx_battle_group_capacity(void *game, int group, int *cap);
 int mfx_battle_rollout_init(void *game, const int *tmpl_n, const int *const *xs, const int *const *ys,
                             int max_steps, float eps, unsigned seed, int stagger);
 int mfx_battle_rollout_step(void *game, int n_steps);
-/* Steps per launch (1..64, default 1; 0 = chosen per path and batch size): k_rollout runs each env's steps
+/* Steps per launch (1..64, up to 1024 on the pipelined few-env path; default 1; 0 = chosen per path and batch
+ * size): k_rollout runs each env's steps
  * back to back with its image resident in LDS; the large-env queue kernel (k_rollout_bigq) runs every env's
  * steps in one launch.  rollout_step(n) gives identical results for every value.  get: the value in force. */
 int mfx_battle_rollout_set_substeps(void *game, int n_sub);

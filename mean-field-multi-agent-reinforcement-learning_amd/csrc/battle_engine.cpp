@@ -260,6 +260,9 @@ public:
     static constexpr int kSmallERows = 16;
     // the pipelined few-env stepper: wave 0 alone steps envs of up to this many agents (k_rollout's threshold)
     static constexpr int kFewWaveMax = 64;
+    // steps per launch: at most 64 (k_rollout, the queue kernel's item lists); the pipelined few-env form's lists
+    // are sized for kMaxPipeSub (its item words' 6 step bits only guard the hand-off, modulo 64)
+    static constexpr int kMaxSub = 64, kMaxPipeSub = 1024;
     static constexpr int kPipeStepPerCu = 4, kPipeObsPerCu = 2;
     int ro_split = kBigSplit;
     hipStream_t ro_str[kMaxSplit] = {};
@@ -1228,10 +1231,16 @@ public:
                     if (ro_bigq) MFX_HIP_THROW(bigq_grid(gp, s.cap, s.acap, Rq, ra.lds_step, &ro_q_grid));
                     ro_bigq = ro_bigq && ro_q_grid > 0;          // (0: not one SPX device of 8 XCDs)
                     if (ro_bigq) {
-                        // per list and parity: one filing per env and step of a launch (<= 64 steps)
-                        // (+ the tickets workgroups hold past the last filing: two per workgroup)
-                        const size_t lcap = (size_t)((E + kXcds - 1) / kXcds) * 64 * (size_t)(n_groups() * chunks) +
-                                            2 * (size_t)ro_q_grid;
+                        // few envs with the env staged in LDS: the pipelined form (a stepper workgroup per env
+                        // steps while the items observe its snapshot) while the steppers leave at least 3 of 4
+                        // of every XCD's workgroups to the items
+                        const char* fp = getenv("MFX_FEW_PIPE");                // A/B only: 0 = off
+                        ra.few_pipe = ra.lds_step && E <= ro_q_grid / 4 && !(fp && atoi(fp) == 0);
+                        // per list and parity: one filing per env and step of a launch (<= 64 steps; the
+                        // pipelined form kMaxPipeSub) (+ the tickets workgroups hold past the last filing: two
+                        // per workgroup)
+                        const size_t lcap = (size_t)((E + kXcds - 1) / kXcds) * (ra.few_pipe ? kMaxPipeSub : 64) *
+                                            (size_t)(n_groups() * chunks) + 2 * (size_t)ro_q_grid;
                         ro_q_items.ensure(2 * kXcds * lcap);
                         ro_q_cnt.ensure(2 * kXcds * kObsCntPad);
                         ro_q_left.ensure(E); ro_q_si.ensure(E); ro_q_done.ensure(kObsCntPad);
@@ -1240,11 +1249,6 @@ public:
                         ra.q_items = ro_q_items.p; ra.q_cnt = ro_q_cnt.p; ra.q_left = ro_q_left.p;
                         ra.q_si = ro_q_si.p; ra.q_done = ro_q_done.p; ra.q_list_cap = lcap;
                         ra.obs_item_rows = Rq;
-                        // few envs with the env staged in LDS: the pipelined form (a stepper workgroup per env
-                        // steps while the items observe its snapshot) while the steppers leave at least 3 of 4
-                        // of every XCD's workgroups to the items
-                        const char* fp = getenv("MFX_FEW_PIPE");                // A/B only: 0 = off
-                        ra.few_pipe = ra.lds_step && E <= ro_q_grid / 4 && !(fp && atoi(fp) == 0);
                         if (ra.few_pipe) {
                             const char* fw = getenv("MFX_FEW_WAVE_MAX");        // A/B only
                             // (at most 64: attack_wave / move_wave give each attacker and mover one lane)
@@ -1497,14 +1501,16 @@ public:
     }
 
     // Steps per launch: ro_sub, or with ro_sub 0 (mfx_battle_rollout_set_substeps(game, 0)) the measured best of the
-    // path (profiles/r04_substeps_auto.txt, one MI355X): the pipelined few-env stepper 64 (the launch ends with
-    // its slowest env's steps, and a longer launch averages each env's heavy early-episode steps with its light
-    // ones: 8 envs 0.0356 -> 0.0285 ms per step from 20 to 64); k_rollout below 96 envs per CU 2 (its workgroups'
+    // path (profiles/r04_substeps_auto.txt, one MI355X): the pipelined few-env stepper kMaxPipeSub -- a launch ends
+    // with its slowest env's steps (the envs step independently inside it), and a longer launch averages each env's
+    // heavy early-episode steps with its light ones: 8 envs 0.0356 -> 0.0285 ms per step from 20 to 64 steps per
+    // launch --, in practice the whole rollout_step(n) as one launch; k_rollout below 96 envs per CU 2 (its workgroups'
     // heaviest units end the launch: 8192 envs 0.556 -> 0.594 of peak, 16384 0.62 -> 0.63), else 20 (32768
     // envs 0.75 at 5, 0.77 at 20; the bench's 131072, 0.84-0.86); the large-env queue kernel 20.
     int sub_steps() const {
-        if (ro_sub > 0) return ro_sub;
-        if (ro_big) return (ro_bigq && ra.few_pipe) ? 64 : 20;
+        const bool pipe = ro_big && ro_bigq && ra.few_pipe;
+        if (ro_sub > 0) return std::min(ro_sub, pipe ? kMaxPipeSub : kMaxSub);
+        if (ro_big) return pipe ? kMaxPipeSub : 20;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -2417,14 +2423,15 @@ MFX_API int mfx_battle_rollout_sum_lanes(void* game, int n_agents, int* lanes) {
     return 0;
 }
 
-// Steps per k_rollout launch (1..64): every env runs that many consecutive steps while its image stays
+// Steps per k_rollout launch (1..64; up to 1024 on the pipelined few-env path, the others run 64 at most): every
+// env runs that many consecutive steps while its image stays
 // in LDS; the large-env queue kernel k_rollout_bigq runs that many steps of every env per launch (its
 // item lists hold one filing per env and step of a launch: lcap in rollout_plan, hence <= 64).
 // rollout_step(n) results are identical for any value (the last step's buffers, the same state); only
 // the launch count changes.  Ignored by the two pipelines (one step per launch).  0: chosen per path and batch
 // (BattleEnv::sub_steps); mfx_battle_rollout_get_substeps reports the value in force.
 MFX_API int mfx_battle_rollout_set_substeps(void* game, int n_sub) {
-    if (n_sub < 0 || n_sub > 64) return mfx::fail("rollout_set_substeps: %d not in 0..64", n_sub);
+    if (n_sub < 0 || n_sub > 1024) return mfx::fail("rollout_set_substeps: %d not in 0..1024", n_sub);
     MFX_ENV(game)->ro_sub = n_sub;
     return 0;
 }

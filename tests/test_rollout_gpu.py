@@ -959,13 +959,13 @@ def test_rollout_lds_step_matches_hbm_step(monkeypatch):
         assert torch.equal(x, y), k
 
 
-@pytest.mark.parametrize("E,S", [(8, 20), (8, 64), (64, 7), (100, 1)])
+@pytest.mark.parametrize("E,S", [(8, 20), (8, 64), (64, 7), (64, 300), (100, 1)])
 def test_rollout_few_pipe_matches_queue_step(E, S, monkeypatch):
     """The pipelined few-env form (RolloutArgs::few_pipe, the default for <= grid / 4 LDS-sized envs: a stepper
     workgroup per env keeps it in LDS and steps while the items observe its snapshot) against the queue kernel's
     step-after-items form (MFX_FEW_PIPE=0): staggered 64x64 envs, 432 steps (every env restarts), every output
     buffer and the per-call ids / positions / hp bit for bit -- E not a multiple of the 8 XCDs, 1 and 7 steps per
-    launch included."""
+    launch included, and 300 (the pipelined form's launches run past the queue kernel's 64)."""
     import torch
     from mfrl_amd.battle import BattleBatch
     N, T = 128, 432
@@ -987,12 +987,13 @@ def test_rollout_few_pipe_matches_queue_step(E, S, monkeypatch):
 
 def test_rollout_substeps_auto_choice():
     """rollout_substeps(0): the engine picks the steps per launch for its path and batch (BattleEngine::sub_steps):
-    64 for the pipelined few-env stepper, 2 for k_rollout below 96 envs per CU, 20 for the large-env queue kernel;
-    an explicit value is reported as given.  The results do not depend on it (test_rollout_substeps_match_single_steps
+    1024 for the pipelined few-env stepper (in practice the whole rollout_step), 2 for k_rollout below 96 envs per
+    CU, 20 for the large-env queue kernel; an explicit value is reported as given (above 64 clamped to 64 off the
+    pipelined path).  The results do not depend on it (test_rollout_substeps_match_single_steps
     and the few-env replays at 20 and 64 steps per launch)."""
     import torch
     from mfrl_amd.battle import BattleBatch
-    cases = ((64, 256, 8, "k_rollout_bigq", 64), (64, 256, 2048, "k_rollout", 2), (256, 4096, 16, "k_rollout_bigq", 20))
+    cases = ((64, 256, 8, "k_rollout_bigq", 1024), (64, 256, 2048, "k_rollout", 2), (256, 4096, 16, "k_rollout_bigq", 20))
     for map_size, agents, E, path, want in cases:
         left, right = bd.block_positions(map_size, agents // 2)
         eng = BattleBatch(map_size, E, stream=torch.cuda.current_stream())
@@ -1002,6 +1003,8 @@ def test_rollout_substeps_auto_choice():
         assert eng.get_substeps() == want, (map_size, E, eng.get_substeps())
         eng.rollout_substeps(7)
         assert eng.get_substeps() == 7
+        eng.rollout_substeps(300)
+        assert eng.get_substeps() == (300 if want == 1024 else 64)
         eng.rollout_substeps(0)
         eng.rollout_step(3)
         eng.rollout_check()
