@@ -88,6 +88,11 @@ int gridworld_add_reward_rule(void *game, int on, int *receiver, float *value, i
  * outgrows them; valid until the step after next or env_delete_game.  Returns 1 (nothing set) when
  * the observation is not held that way -- call env_get_observation then. */
 int mfx_env_observation_view(void *game, int group, float **view, float **feature, int *n, int *rows);
+/* Extension of env_get_info("num") + env_get_info("id" / "alive" / "pos") / env_get_reward (runtime_api.h:125-127)
+ * for the drop-in python: one call per getter.  Returns the group's agent count n and, when n <= cap, copies
+ * its n rows of field `what` (0 id int32, 1 reward float32, 2 alive uint8, 3 pos int32 x 2; -1: the count only)
+ * into out; -1 on error. */
+int mfx_env_get_rows(void *game, int group, int what, void *out, int cap);
 
 /* ---------------------------------------------------------------- part 2: batched Battle */
 /* Before the first env_reset: make the engine hold n_envs identical envs. */

@@ -1985,6 +1985,22 @@ public:
         return check_err();
     }
 
+    // One call per getter of the drop-in wrapper (mfx_env_get_rows): the group's size n, and for what 0 id /
+    // 1 reward / 2 alive / 3 pos the n rows copied into out when n <= cap (what -1: the size only).
+    int get_rows(int g, int what, void* out, int cap) {
+        MFX_CHECK(sync_cells());
+        if (g < 0 || g >= n_groups()) return fail("get_rows: bad group %d", g);
+        if (what < -1 || what > 3) return fail("get_rows: bad field %d", what);
+        if (!allocated) return 0;
+        MFX_CHECK(ensure_counts());
+        const int n = hn[g];
+        if (what < 0 || n == 0 || n > cap) return n;
+        static const int field[4] = {kGetId, kGetReward, kGetAlive, kGetPos};
+        static const size_t bytes[4] = {4, 4, 1, 8};
+        MFX_CHECK(host_get(g, field[what], out, bytes[what]));
+        return n;
+    }
+
     int get_info(int group, const char* name, void* buf) {   // GridWorld.cc:777-978
         int* ib = (int*)buf;
         const int G = n_groups();
@@ -2272,6 +2288,13 @@ MFX_API int env_get_reward(void* game, int group, float* buffer) {
 }
 MFX_API int env_get_info(void* game, int group, const char* name, void* buffer) {
     MFX_GUARD(MFX_ENV(game)->get_info_global(group, name, buffer));
+}
+// The drop-in wrapper's getters in one FFI call each where the reference's wrapper makes two
+// (gridworld.py get_agent_id / get_reward / get_alive / get_pos: env_get_info("num"), then env_get_info(name) or
+// env_get_reward): returns the group's size n and, when n <= cap, copies its n rows of field `what` (0 id int32,
+// 1 reward float32, 2 alive uint8, 3 pos int32 pairs; -1: the size only) into out.  -1 on error.
+MFX_API int mfx_env_get_rows(void* game, int group, int what, void* out, int cap) {
+    MFX_GUARD(MFX_ENV(game)->get_rows(group, what, out, cap));
 }
 MFX_API int env_render(void* game) { MFX_GUARD(MFX_ENV(game)->render()); }
 MFX_API int env_render_next_file(void* game) { MFX_GUARD((MFX_ENV(game)->next_file(), 0)); }

@@ -84,6 +84,7 @@ class Library:
                 raise EngineError("%s failed (%d): %s" % (name, ret, msg))
             return ret
         checked.__name__ = name
+        setattr(self, name, checked)         # made once per function: later calls skip __getattr__
         return checked
 
 

@@ -100,6 +100,13 @@ class GridWorld(Environment):
             self._ov_out = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32(), ctypes.c_int32())
             self._ov_ref = tuple(ctypes.byref(x) for x in self._ov_out)
             self._ov_blocks = {}                 # (address, rows, shape) -> array over that pinned block
+        # engines holding env 0's record on the host answer each getter in one call (mfx_env_get_rows) where
+        # the reference's wrapper makes two (env_get_info("num"), then the field)
+        self._rows = getattr(L.dll, "mfx_env_get_rows", None) if hasattr(L, "dll") else None
+        if self._rows is not None:
+            self._rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+            self._rows.restype = ctypes.c_int
+            self._rows_cap = 256
         self.view_space, self.feature_space, self.action_space = {}, {}, {}
         buf = np.empty((3,), dtype=np.int32)
         for h in self.group_handles:
@@ -215,6 +222,8 @@ class GridWorld(Environment):
         return bool(done.value)
 
     def get_reward(self, handle):
+        if self._rows is not None:
+            return self._get_rows(handle, 1, np.float32)
         buf = np.empty((self.get_num(handle),), dtype=np.float32)
         self._lib.env_get_reward(self.game, _hv(handle), as_float_c_array(buf))
         return buf
@@ -226,7 +235,24 @@ class GridWorld(Environment):
     def get_handles(self):
         return self.group_handles
 
+    def _get_rows(self, handle, what, dtype, tail=()):
+        """A fresh array of the group's rows of field `what` (mfx_env_get_rows: 0 id, 1 reward, 2 alive, 3 pos)."""
+        g = _hv(handle)
+        while True:
+            buf = np.empty((self._rows_cap,) + tail, dtype=dtype)
+            n = self._rows(self.game, g, what, buf.__array_interface__["data"][0], self._rows_cap)
+            if n < 0:
+                raise EngineError("mfx_env_get_rows failed: %s" % self._lib.dll.mfx_last_error().decode())
+            if n <= self._rows_cap:
+                return buf[:n]
+            self._rows_cap = max(n, 2 * self._rows_cap)
+
     def get_num(self, handle):
+        if self._rows is not None:
+            n = self._rows(self.game, _hv(handle), -1, None, 0)
+            if n < 0:
+                raise EngineError("mfx_env_get_rows failed: %s" % self._lib.dll.mfx_last_error().decode())
+            return n
         num = ctypes.c_int32()
         self._lib.env_get_info(self.game, _hv(handle), b"num", ctypes.byref(num))
         return num.value
@@ -246,12 +272,18 @@ class GridWorld(Environment):
         return buf
 
     def get_agent_id(self, handle):
+        if self._rows is not None:
+            return self._get_rows(handle, 0, np.int32)
         return self._info_array(handle, b"id", (self.get_num(handle),), np.int32)
 
     def get_alive(self, handle):
+        if self._rows is not None:
+            return self._get_rows(handle, 2, np.bool_)
         return self._info_array(handle, b"alive", (self.get_num(handle),), np.bool_)
 
     def get_pos(self, handle):
+        if self._rows is not None:
+            return self._get_rows(handle, 3, np.int32, (2,))
         return self._info_array(handle, b"pos", (self.get_num(handle), 2), np.int32)
 
     def get_view2attack(self, handle):
