@@ -20,6 +20,10 @@ python3 -c "import json; d=json.load(open('$O/bench_${E}envs.json')); print('$E 
 done
 timeout -k 10 300 python bench.py --gpus 2 --backend gloo --envs 2048 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_2rank.json 2> $O/bench_2rank.err || { tail -20 $O/bench_2rank.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_2rank.json')); print('2 ranks', d['n_gpus'], d['ranks'], d['config']['parallelism'], d['episodes']['note'])"
+timeout -k 10 300 python bench.py --gpus 2 --backend gloo --total-envs 16 --steps 256 --warmup 64 --no-cpu-baseline > $O/bench_2rank_16envs.json 2> $O/bench_2rank_16envs.err || { tail -20 $O/bench_2rank_16envs.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench_2rank_16envs.json')); print('2 ranks x 8 envs', '%.4e' % d['value'], 'ms/step %.4f' % d['ms_per_step'], d['config']['parallelism'], 'check', d['check']['ok'])"
+timeout -k 10 200 python scripts/bench_dropin.py --map 40 --agents 128 --seconds 4 --calls > $O/dropin_40.json 2> $O/err || { tail -20 $O/err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/dropin_40.json')); print('drop-in 40x40 vs ref', '%.3f' % d['hip_vs_ref'])"
 for P in qnet mfac; do
 timeout -k 10 300 python bench.py --policy $P --no-cpu-baseline > $O/bench_$P.json 2> $O/err || { tail -20 $O/err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_$P.json')); print('$P', '%.4e' % d['value'], 'frac %.4f' % d['roofline']['frac'])"
