@@ -447,6 +447,13 @@ def main():
             with _StdoutToStderr():
                 dist.init_process_group(args.backend)
     E = rank_envs(args, world, rank)
+    if world > n_gpus:
+        # ranks sharing a card (the gloo rehearsal): the queue kernels' in-launch hand-offs assume their whole
+        # persistent grid is resident on the GPU (one process per GPU, as under RCCL), which two processes'
+        # grids on one card do not guarantee -- few envs take k_rollout here instead, large envs the two-stream
+        # pipeline (neither waits on other workgroups of its launch)
+        os.environ["MFX_SMALL_E"] = "0"
+        os.environ["MFX_BIG_FUSED"] = "0"
     stream = torch.cuda.current_stream()
     left, right = bd.block_positions(args.map, args.agents // 2)
     from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing
@@ -537,7 +544,9 @@ def main():
             "data": "synthetic (fixed-seed two-block placement, on-device rush policy)",
             "config": {"workload": "Battle %dx%d, %d+%d agents, %s, episode cap %d, %s"
                        % (args.map, args.map, args.agents // 2, args.agents // 2,
-                          ("%d envs over %d GPUs" % (args.total_envs, world)) if strong else "%d envs per GPU" % E,
+                          (("%d envs over %d GPUs" % (args.total_envs, world)) if n_gpus == world else
+                           ("%d envs over %d ranks on %d GPU(s)" % (args.total_envs, world, n_gpus))) if strong else
+                          "%d envs per GPU" % E if n_gpus == world else "%d envs per rank" % E,
                           args.max_steps,
                           ("%s, %d steps per launch" % (path, S_run)) if big else
                           ("fused step" if S_run == 1 else "fused step, %d consecutive steps per launch" % S_run)),
