@@ -18,6 +18,7 @@
 #include <sstream>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
 #include <vector>
@@ -28,6 +29,35 @@
 #include "../../include/magent_amd.h"
 
 namespace mfx {
+
+// The queue kernels (k_rollout_bigq) hand work between the workgroups of one launch and wait on each other, which
+// needs their whole persistent grid resident: one process per GPU guarantees it for one launch at a time, and this
+// lock keeps the process's own engines (several on one device, on different streams) from running two of them at
+// once -- each bigq launch waits for the previous one's completion event on its device.  (Two processes sharing a
+// card are outside that; bench.py routes its gloo rehearsals off these kernels.)
+class BigqSerial {
+  public:
+    explicit BigqSerial(hipStream_t st) : st_(st), lock_(mu()) {
+        if (hipGetDevice(&dev_) != hipSuccess || dev_ < 0 || dev_ >= kDevs) dev_ = -1;
+        else if (has()[dev_]) err_ = hipStreamWaitEvent(st_, ev()[dev_], 0);
+    }
+    ~BigqSerial() {
+        if (dev_ < 0) return;
+        if (!ev()[dev_] && hipEventCreateWithFlags(&ev()[dev_], hipEventDisableTiming) != hipSuccess) return;
+        if (hipEventRecord(ev()[dev_], st_) == hipSuccess) has()[dev_] = true;
+    }
+    hipError_t status() const { return err_; }
+
+  private:
+    static constexpr int kDevs = 64;
+    static std::mutex& mu() { static std::mutex m; return m; }
+    static hipEvent_t* ev() { static hipEvent_t e[kDevs] = {}; return e; }
+    static bool* has() { static bool h[kDevs] = {}; return h; }
+    hipStream_t st_;
+    std::lock_guard<std::mutex> lock_;
+    int dev_ = -1;
+    hipError_t err_ = hipSuccess;
+};
 
 // ------------------------------------------------------------------ host-side ranges
 struct HostRange {                                  // Range.h:14-113
@@ -1341,6 +1371,8 @@ public:
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, lst * sizeof(int32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_step.p, 0, kXcds * sizeof(int32_t), stream));
                 ro_qdone += (uint32_t)E * (uint32_t)k;
+                BigqSerial serial(stream);
+                MFX_HIP(serial.status());
                 MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, 0,
                                             qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
                                             ra.lds_step, stream, true));
@@ -1373,6 +1405,8 @@ public:
                 const int k = std::min(sub_steps(), n_steps - i);
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p + (ro_qpar ^ 1) * lst, 0, lst * sizeof(int32_t), stream));
                 ro_qdone += (uint32_t)E * (uint32_t)k;
+                BigqSerial serial(stream);
+                MFX_HIP(serial.status());
                 MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, ro_qpar,
                                             qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
                                             ra.lds_step, stream));

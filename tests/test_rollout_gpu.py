@@ -1009,3 +1009,33 @@ def test_rollout_substeps_auto_choice():
         eng.rollout_step(3)
         eng.rollout_check()
         del eng
+
+
+@pytest.mark.parametrize("E", [8, 64])
+def test_rollout_two_engines_two_streams(E):
+    """Two engines on two streams of one device, both on the pipelined few-env path, their launches enqueued back to
+    back: the queue kernels need their whole persistent grid resident, so the engine serialises them process-wide
+    (BigqSerial) instead of letting two grids share the card -- both finish without a stalled wait (rollout_check)
+    and, seeded alike, leave identical buffers."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    N = 128
+    left, right = bd.block_positions(64, N)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    engs = []
+    for st in streams:
+        eng = BattleBatch(64, E, stream=st)
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=2468, stagger=True)
+        eng.rollout_substeps(0)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        engs.append(eng)
+    for _ in range(3):
+        for eng in engs:
+            eng.rollout_step(150)
+    torch.cuda.synchronize()
+    dumps = []
+    for eng in engs:
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, N))
+    for (k, x), (_, y) in zip(dumps[0], dumps[1]):
+        assert torch.equal(x, y), k
