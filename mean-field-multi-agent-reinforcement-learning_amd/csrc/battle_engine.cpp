@@ -1289,6 +1289,13 @@ public:
                             ro_snap.ensure((size_t)E * 2 * ra.few_snap_bytes);
                             ro_q_step.ensure(kXcds);
                             ra.few_snap = ro_snap.p; ra.q_step = ro_q_step.p;
+                            // one workgroup per CU while that leaves 3 of 4 to the items: the stepper then has its
+                            // CU to itself (8 envs 0.0222 -> 0.0219 ms per step, profiles/r04_few_grid_ab.txt)
+                            int dev = 0, cus = 0;
+                            if (hipGetDevice(&dev) == hipSuccess &&
+                                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                                cus % kXcds == 0 && 4 * E <= cus)
+                                ro_q_grid = std::min(ro_q_grid, cus);
                         }
                         const char* qg = getenv("MFX_BIGQ_GRID");               // sweeps only
                         // (a multiple of kXcds: every XCD's list needs workgroups of its own)
