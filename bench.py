@@ -480,10 +480,11 @@ def main():
     eng.rollout_step(args.max_steps + args.warmup)
     torch.cuda.synchronize()
 
-    # launches of the timed region: S steps each (the last one the remainder); HIP events around each
-    # launch on the engine's stream
+    # launches of the timed region: S steps each (the last one the remainder); HIP events on the engine's
+    # stream around the whole region (an event pair around every launch put two timestamp packets between
+    # consecutive launches: at 8192 envs x 2 steps per launch ~5 % of the wall time went to them)
     chunks = [min(S, args.steps - k) for k in range(0, args.steps, S)]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in chunks]
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     a0 = agent_steps()
     if world > 1:
         dist.barrier()
@@ -491,15 +492,15 @@ def main():
     t0 = time.perf_counter()
     red = None
     done_steps = 0
+    ev[0].record(stream)
     for k, n in enumerate(chunks):
-        ev[k][0].record(stream)
         eng.rollout_step(n)
-        ev[k][1].record(stream)
         done_steps += n
         # episode statistics -> RCCL all-reduce, once per episode batch (an episode cap of steps) and at
         # the end of the timed window: the only collective
         if world > 1 and (done_steps // args.max_steps != (done_steps - n) // args.max_steps or k == len(chunks) - 1):
             red = reduce_stats(stats())
+    ev[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -508,19 +509,16 @@ def main():
     if red is None:                  # one rank: the same statistics, reduced after the clock
         red = reduce_stats(stats())
     red = red.tolist()
-    launch_ms = [s.elapsed_time(e) for s, e in ev]
-    # per-launch average over the full-size launches (a shorter remainder launch would skew it)
-    full = [t for t, n in zip(launch_ms, chunks) if n == S] or launch_ms
-    kernel_ms = sum(full) / len(full)
+    # the mean launch of the timed region (its launches back to back on the stream: the region / their count)
+    kernel_ms = ev[0].elapsed_time(ev[1]) / len(chunks)
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
     check = run_check(eng, args, E, [left, right], env_seed(1234, rank), world)
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
-        # agent-steps of one launch the kernel_ms average covers (full-size launches, else all of them)
-        steps_per_timed_launch = S if any(n == S for n in chunks) else args.steps / len(chunks)
+        steps_per_timed_launch = args.steps / len(chunks)       # the mean launch kernel_ms is
         S_run = max(chunks)                  # the launches of the timed region (S caps them at K steps)
-        units_per_launch = local_units / args.steps * steps_per_timed_launch
+        units_per_launch = local_units / len(chunks)
         achieved = BYTES_PER_AGENT_STEP * units_per_launch / (kernel_ms * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_big256.json" if big else "pmc_k_rollout.json")
@@ -559,8 +557,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kernel_ms,
-                         "kernel_ms_is": "mean launch duration (HIP events on the launch stream), %g step(s) per launch"
-                                         % steps_per_timed_launch,
+                         "kernel_ms_is": "mean launch duration: HIP events on the launch stream around the timed "
+                                         "region's %d launch(es), / their count; %g step(s) per launch"
+                                         % (len(chunks), steps_per_timed_launch),
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch,
                          "grid": grid, "lds_bytes": lds},
             "cpu_baseline": None,
