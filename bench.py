@@ -447,13 +447,8 @@ def main():
             with _StdoutToStderr():
                 dist.init_process_group(args.backend)
     E = rank_envs(args, world, rank)
-    if world > n_gpus:
-        # ranks sharing a card (the gloo rehearsal): the queue kernels' in-launch hand-offs assume their whole
-        # persistent grid is resident on the GPU (one process per GPU, as under RCCL), which two processes'
-        # grids on one card do not guarantee -- few envs take k_rollout here instead, large envs the two-stream
-        # pipeline (neither waits on other workgroups of its launch)
-        os.environ["MFX_SMALL_E"] = "0"
-        os.environ["MFX_BIG_FUSED"] = "0"
+    # (ranks sharing a card -- the gloo rehearsal -- run the same kernels as one rank per GPU: the queue kernels
+    # complete with one resident workgroup per XCD, DESIGN.md §5 "Forward progress")
     stream = torch.cuda.current_stream()
     left, right = bd.block_positions(args.map, args.agents // 2)
     from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing

@@ -30,11 +30,13 @@
 
 namespace mfx {
 
-// The queue kernels (k_rollout_bigq) hand work between the workgroups of one launch and wait on each other, which
-// needs their whole persistent grid resident: one process per GPU guarantees it for one launch at a time, and this
-// lock keeps the process's own engines (several on one device, on different streams) from running two of them at
-// once -- each bigq launch waits for the previous one's completion event on its device.  (Two processes sharing a
-// card are outside that; bench.py routes its gloo rehearsals off these kernels.)
+// The queue kernels (k_rollout_bigq) hand work between the workgroups of one launch.  Each env lives on one XCD, an
+// XCD's work of a launch completes with any one of the launch's workgroups resident there, and a workgroup leaves as
+// soon as its XCD's work is done (rollout_big.inc xcd_done); the pipelined few-env form also claims stepper roles and
+// takes back unclaimed items from waiting workgroups (few_rollout).  So neither needs its whole grid co-resident.
+// The large-env form still runs one launch at a time per process and device (this lock: each such launch waits for
+// the previous one's completion event on its device) -- its grid fills every CU, and two of them dispatched at once
+// would split the chip between two copies of the same observation stream for no gain.
 class BigqSerial {
   public:
     explicit BigqSerial(hipStream_t st) : st_(st), lock_(mu()) {
@@ -255,7 +257,7 @@ public:
     DevBuf<int32_t> ro_q_step;               // few_pipe: [kXcds] stepper claims
     DevBuf<int32_t> ro_q_cnt, ro_q_left, ro_q_done;
     int ro_q_grid = 0, ro_qpar = 0;
-    uint32_t ro_qlaunch = 0, ro_qdone = 0;   // launches so far (item tags); env-steps the queue has done
+    uint32_t ro_qlaunch = 0;                 // launches so far (item tags)
     static uint32_t qtag(uint32_t launch) { return launch % 63u + 1u; }   // 6 tag bits (rollout_big.inc), never 0
     bool ro_prep_stale = true;               // ro_mm / ro_info / items lag the state (per-call calls since)
     DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
@@ -1265,7 +1267,15 @@ public:
                         // steps while the items observe its snapshot) while the steppers leave at least 3 of 4
                         // of every XCD's workgroups to the items
                         const char* fp = getenv("MFX_FEW_PIPE");                // A/B only: 0 = off
-                        ra.few_pipe = ra.lds_step && E <= ro_q_grid / 4 && !(fp && atoi(fp) == 0);
+                        ra.few_pipe = ra.lds_step && E <= ro_q_grid / 4 && !(fp && atoi(fp) == 0) &&
+                                      bigq_smem_bytes(gp, s.cap, s.acap, Rq, true, true) <= 160 * 1024;
+                        if (ra.few_pipe) {
+                            // (the stepper's scratch for the items it takes back follows its LDS layout)
+                            int pg = 0;
+                            MFX_HIP_THROW(bigq_grid(gp, s.cap, s.acap, Rq, true, &pg, true));
+                            ro_q_grid = std::min(ro_q_grid, pg);
+                            ra.few_pipe = E <= ro_q_grid / 4;
+                        }
                         // per list and parity: one filing per env and step of a launch (<= 64 steps; the
                         // pipelined form kMaxPipeSub) (+ the tickets workgroups hold past the last filing: two
                         // per workgroup)
@@ -1366,7 +1376,6 @@ public:
             MFX_CHECK(sync_cells());
             const size_t lst = (size_t)kXcds * kObsCntPad;
             if (ro_prep_stale) {
-                ro_qdone = 0;
                 ro_qlaunch++;
                 MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
@@ -1375,13 +1384,17 @@ public:
             ro_prep_stale = false;
             for (int i = 0; i < n_steps;) {
                 const int k = std::min(sub_steps(), n_steps - i);
-                MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, lst * sizeof(int32_t), stream));
+                // a slot whose item its stepper took back keeps the stolen mark if no holder reached it before the
+                // launch ended (k_rollout_bigq: bigq_wait / few_steal): clear the lists when the tag comes round
+                if (qtag(ro_qlaunch) == 1)
+                    MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
+                // (both parities: parity 1 holds the per-XCD done counts, k_rollout_bigq xcd_done)
+                MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, 2 * lst * sizeof(int32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_step.p, 0, kXcds * sizeof(int32_t), stream));
-                ro_qdone += (uint32_t)E * (uint32_t)k;
-                BigqSerial serial(stream);
-                MFX_HIP(serial.status());
+                // (no BigqSerial: the pipelined form completes with one workgroup of its grid per XCD, and its grid
+                // -- one or two workgroups per CU, at most half of an XCD's slots -- never holds a whole XCD)
                 MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, 0,
-                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
+                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), ro_q_grid,
                                             ra.lds_step, stream, true));
                 ro_qlaunch++;
                 ro_launch++;
@@ -1398,7 +1411,6 @@ public:
                 // consumed) still hold the live tag in the slots past the new, smaller filing count --
                 // clear every slot and move to a fresh tag, so no stale word can pass for an item.
                 ro_qpar = 0;
-                ro_qdone = 0;
 #ifndef MFX_AB_R2_RESEED                 // A/B only: the round-2 re-seed, which the regression test must catch
                 ro_qlaunch++;
                 MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
@@ -1411,11 +1423,10 @@ public:
             for (int i = 0; i < n_steps;) {
                 const int k = std::min(sub_steps(), n_steps - i);
                 MFX_HIP(hipMemsetAsync(ro_q_cnt.p + (ro_qpar ^ 1) * lst, 0, lst * sizeof(int32_t), stream));
-                ro_qdone += (uint32_t)E * (uint32_t)k;
                 BigqSerial serial(stream);
                 MFX_HIP(serial.status());
                 MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, ro_qpar,
-                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), (int32_t)ro_qdone, ro_q_grid,
+                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), ro_q_grid,
                                             ra.lds_step, stream));
                 ro_qpar ^= 1;
                 ro_qlaunch++;

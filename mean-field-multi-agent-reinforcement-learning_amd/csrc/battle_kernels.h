@@ -47,14 +47,14 @@ hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, cons
 hipError_t rollout_grid(const GameParams& gp, const State& s, int rows, int split, int per_cu_want, int* grid);
 // large envs, one queue-driven launch per n_sub steps (k_rollout_bigq)
 // lds_env: the few-env path stages each env in LDS for its step (RolloutArgs::lds_step)
-size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows, bool lds_env);
-hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, bool lds_env, int* grid);
+size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows, bool lds_env, bool pipe = false);
+hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, bool lds_env, int* grid, bool pipe = false);
 hipError_t launch_bigq_seed(const GameParams* d_gp, const State& s, const RolloutArgs& ra, int par, uint32_t tag,
                             uint32_t step_index, hipStream_t st);
 // pipe: the pipelined few-env form (RolloutArgs::few_pipe: one stepper workgroup per env, k_rollout_bigq<true>)
 hipError_t launch_rollout_bigq(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                                int rows, uint32_t si0, int n_sub, int par, uint32_t tag_cur, uint32_t tag_next,
-                               int32_t done_target, int grid, bool lds_env, hipStream_t st, bool pipe = false);
+                               int grid, bool lds_env, hipStream_t st, bool pipe = false);
 size_t few_snap_bytes(int cells_n, int cap, int G);
 size_t rollout_reset_image_bytes(const GameParams& gp, int cells_n, int cap);
 hipError_t launch_reset_image(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutArgs& ra,

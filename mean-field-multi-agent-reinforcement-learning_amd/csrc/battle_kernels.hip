@@ -302,19 +302,23 @@ hipError_t launch_rollout_big(const GameParams& gp, const GameParams* d_gp, cons
     return hipGetLastError();
 }
 
-size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows, bool lds_env) {
+// The step's layout and an item's observation scratch share the LDS (a workgroup does one or the other), except in
+// the pipelined form, where a stepper observes the items it took back (few_stolen) with its env still in LDS: the
+// scratch then follows the step's layout.
+size_t bigq_smem_bytes(const GameParams& gp, int cap, int acap, int rows, bool lds_env, bool pipe) {
     const size_t a = big_step_smem_bytes(gp, cap, acap, true, lds_env);
     const size_t b = obs_smem_core(gp, 0, 0, rows, obs_stage_floats(gp, 0, true, kBigRolloutThreads), true);
-    return a > b ? a : b;
+    return pipe ? a + b : a > b ? a : b;
 }
 
-hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, bool lds_env, int* grid) {
-    const size_t smem = bigq_smem_bytes(gp, cap, acap, rows, lds_env);
+hipError_t bigq_grid(const GameParams& gp, int cap, int acap, int rows, bool lds_env, int* grid, bool pipe) {
+    const size_t smem = bigq_smem_bytes(gp, cap, acap, rows, lds_env, pipe);
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t err = hipGetDevice(&dev);
     if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (err == hipSuccess)
-        err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rollout_bigq<false>, kBigRolloutThreads, smem);
+        err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pipe ? k_rollout_bigq<true> : k_rollout_bigq<false>,
+                                                           kBigRolloutThreads, smem);
     if (err != hipSuccess) return err;
     // one device of all 8 XCDs (SPX, 32 CUs each): every XCD gets workgroups of the full-occupancy grid,
     // and the XCC ids are 0-7 (k_rollout_bigq keeps each env on XCD e % 8)
@@ -330,15 +334,13 @@ hipError_t launch_bigq_seed(const GameParams* d_gp, const State& s, const Rollou
 
 hipError_t launch_rollout_bigq(const GameParams& gp, const GameParams* d_gp, const State& s, const RolloutCtx* d_ctx,
                                int rows, uint32_t si0, int n_sub, int par, uint32_t tag_cur, uint32_t tag_next,
-                               int32_t done_target, int grid, bool lds_env, hipStream_t st, bool pipe) {
-    const size_t smem = bigq_smem_bytes(gp, s.cap, s.acap, rows, lds_env);
+                               int grid, bool lds_env, hipStream_t st, bool pipe) {
+    const size_t smem = bigq_smem_bytes(gp, s.cap, s.acap, rows, lds_env, pipe);
     if (smem > 160 * 1024 || grid < 1 || n_sub < 1 || (pipe && !lds_env)) return hipErrorInvalidValue;
     if (pipe)
-        k_rollout_bigq<true><<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
-                                                                    done_target);
+        k_rollout_bigq<true><<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next);
     else
-        k_rollout_bigq<false><<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next,
-                                                                     done_target);
+        k_rollout_bigq<false><<<grid, kBigRolloutThreads, smem, st>>>(d_gp, d_ctx, si0, n_sub, par, tag_cur, tag_next);
     return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ the reference attack loop is racy with more threads.
 
 Output: tests/golden/battle_*.npz (numeric arrays only, no pickles) + manifest.json.
 
-    OMP_NUM_THREADS=1 python tests/golden/make_battle_fixtures.py battle256_seq battle256_rollout
+    OMP_NUM_THREADS=1 python tests/golden/make_battle_fixtures.py battle256_rollout battle64_rollout
 
 regenerates only the named cases (the manifest's other entries are kept).
 """
@@ -133,6 +133,8 @@ def main(only=()):
         case_battle256_seq(new_env, manifest)
     if want("battle256_rollout"):
         case_battle256_rollout(new_env, manifest)
+    if want("battle64_rollout"):
+        case_battle64_rollout(new_env, manifest)
 
     with open(os.path.join(HERE, "battle_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
@@ -266,19 +268,34 @@ def case_battle256_seq(new_env, manifest):
                                           "note": "two full episodes in one env (band mode, LCG persistence)"}
 
 
-def case_battle256_rollout(new_env, manifest, E=2048, seed=1234, eps=0.2, max_steps=400, episodes=2):
-    # 6) env 0 of the 256x256 bench batch (bench.py: E staggered envs, env 0 starts at episode length 0)
-    #    under the DEVICE rush policy (tests/rollout_check.py device_rush_actions: a counter hash of
-    #    seed / env / step / id), recorded on the reference engine through the reference wrapper: a
-    #    k_rollout_bigq launch of that batch must reproduce it at every launch boundary.
+def case_battle256_rollout(new_env, manifest):
+    # 6) env 0 of the 256x256 bench batch (bench.py: 2048 staggered envs) -- k_rollout_bigq's reference pin
+    case_rollout(new_env, manifest, "battle256_rollout", 256, 2048, E=2048)
+
+
+def case_battle64_rollout(new_env, manifest):
+    # 7) env 0 of the 64x64 bench batch (bench.py: 131072 staggered envs, the metric's config) -- k_rollout's
+    #    reference pin; also the first env of every smaller batch (configs[3]'s 8 per GPU)
+    case_rollout(new_env, manifest, "battle64_rollout", 64, 128, E=131072)
+
+
+def case_rollout(new_env, manifest, name, map_size, n_side, E, seed=1234, eps=0.2, max_steps=400, episodes=2):
+    # env 0 of a staggered bench batch (env 0 starts at episode length 0 for any batch size) under the DEVICE rush
+    # policy (tests/rollout_check.py device_rush_actions: a counter hash of seed / env / step / id), recorded on the
+    # reference engine through the reference wrapper: a fused rollout of that batch must reproduce it at every launch
+    # boundary.  The reward sums are recorded in the device's orders for 64-, 256- and 512-lane teams (the engine
+    # reports which team sums an env-step of n agents: BattleBatch.rollout_sum_lanes).
     import rollout_check as rck
-    env, h = new_env(256)
-    placement = bd.placement_blocks(256, 2048)
+    env, h = new_env(map_size)
+    placement = bd.placement_blocks(map_size, n_side)
     G = len(h)
     n_action = int(env.get_action_space(h[0])[0])
     attack_base, v2a = env.get_view2attack(h[0])
+    lanes = (64, 256, 512)
     rec = {k: [] for k in ("n", "sha_view", "sha_feat", "sha_ids", "sha_reward", "sha_alive", "sha_pos",
-                           "sha_ids_cd", "sha_pos_cd", "num_after", "done", "rsum512", "ep_len")}
+                           "sha_ids_cd", "sha_pos_cd", "num_after", "done", "ep_len")}
+    for L in lanes:
+        rec["rsum%d" % L] = []
     acts_all = []
 
     def reset():
@@ -304,7 +321,8 @@ def case_battle256_rollout(new_env, manifest, E=2048, seed=1234, eps=0.2, max_st
         rec["sha_reward"].append([bd.sha(r) for r in rew])
         rec["sha_alive"].append([bd.sha(env.get_alive(h[g])) for g in range(G)])
         rec["sha_pos"].append([bd.sha(env.get_pos(h[g])) for g in range(G)])
-        rec["rsum512"].append([rck.device_sum(r, 512) for r in rew])
+        for L in lanes:
+            rec["rsum%d" % L].append([rck.device_sum(r, L) for r in rew])
         rec["done"].append(bool(done))
         acts_all.append(acts)
         env.clear_dead()
@@ -319,19 +337,20 @@ def case_battle256_rollout(new_env, manifest, E=2048, seed=1234, eps=0.2, max_st
             reset()
         t += 1
     out = {"n": np.array(rec["n"], dtype=np.int32), "num_after": np.array(rec["num_after"], dtype=np.int32),
-           "done": np.array(rec["done"], dtype=np.bool_), "rsum512": np.array(rec["rsum512"], dtype=np.float32),
-           "ep_len": np.array(rec["ep_len"], dtype=np.int32),
+           "done": np.array(rec["done"], dtype=np.bool_), "ep_len": np.array(rec["ep_len"], dtype=np.int32),
            "actions": np.concatenate([a for row in acts_all for a in row]).astype(np.int8)}
+    for L in lanes:
+        out["rsum%d" % L] = np.array(rec["rsum%d" % L], dtype=np.float32)
     for k in ("sha_view", "sha_feat", "sha_ids", "sha_reward", "sha_alive", "sha_pos", "sha_ids_cd", "sha_pos_cd"):
         out[k] = np.frombuffer(b"".join(b for row in rec[k] for b in row), dtype=np.uint8).reshape(t, G, 32)
     del env
-    np.savez_compressed(os.path.join(HERE, "battle256_rollout.npz"), **out)
-    manifest["cases"]["battle256_rollout"] = {
-        "map_size": 256, "placement": "blocks2048", "steps": t, "env": 0, "n_envs": E, "seed": seed, "eps": eps,
-        "max_steps": max_steps, "episodes": episodes,
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    manifest["cases"][name] = {
+        "map_size": map_size, "placement": "blocks%d" % n_side, "steps": t, "env": 0, "n_envs": E, "seed": seed,
+        "eps": eps, "max_steps": max_steps, "episodes": episodes, "sum_lanes": list(lanes),
         "note": "env 0 of the staggered bench batch under the device rush policy; per step: obs / ids / "
                 "rewards / alive / pos hashes, post-clear_dead ids / pos hashes, actions, reward sums in the "
-                "512-lane device order"}
+                "64-, 256- and 512-lane device orders"}
 
 
 if __name__ == "__main__":

@@ -294,9 +294,12 @@ class RolloutChecker:
 # env 0 of the 256x256 bench batch under the device rush policy, recorded on the reference engine itself
 # --------------------------------------------------------------------------------------------------------
 class RolloutFixture:
-    """Expected per-launch-boundary records of env `case["env"]` from the reference recording."""
+    """Expected per-launch-boundary records of env `case["env"]` from the reference recording
+    (battle256_rollout: the 256x256 bench batch; battle64_rollout: the 64x64 one).  lanes: the engine's reward-sum
+    teams (BattleBatch.rollout_sum_lanes for <= 64 and > 64 agents); the recording holds the sums in every team
+    order the engines use, and the running episode return follows the one the engine takes at each step."""
 
-    def __init__(self, name="battle256_rollout"):
+    def __init__(self, name="battle256_rollout", lanes=(512, 512)):
         self.case = common.manifest()["cases"][name]
         self.fx = np.load(common.GOLDEN + "/" + name + ".npz")
         self.n = self.fx["n"]
@@ -310,7 +313,8 @@ class RolloutFixture:
         st, ret = np.zeros(4, dtype=np.float64), np.zeros(self.n.shape[1], dtype=np.float32)
         self.restart = np.zeros(T, dtype=bool)
         for t in range(T):
-            ret = (ret + self.fx["rsum512"][t]).astype(np.float32)
+            L = lanes[0] if int(self.n[t].sum()) <= 64 else lanes[1]
+            ret = (ret + self.fx["rsum%d" % L][t]).astype(np.float32)
             st[3] += float((self.n[t] - self.fx["num_after"][t]).sum())
             if self.fx["done"][t] or self.fx["ep_len"][t] >= self.case["max_steps"]:
                 self.restart[t] = True

@@ -52,14 +52,18 @@ def test_oracle_replays_reference_full_large_episodes(name):
     assert common.replay_case(common.ORACLE_LIB, name) == []
 
 
-def test_oracle_replays_reference_rollout_fixture():
-    """Env 0 of the 256x256 bench batch under the device rush policy (restated on the host), two
-    episodes, on the C oracle: every step equals the reference recording (tests/golden/battle256_rollout)."""
+@pytest.mark.parametrize("name,lanes", [("battle256_rollout", (512, 512)), ("battle64_rollout", (64, 256)),
+                                        ("battle64_rollout", (64, 512))])
+def test_oracle_replays_reference_rollout_fixture(name, lanes):
+    """Env 0 of the 256x256 / 64x64 bench batch under the device rush policy (restated on the host), two
+    episodes, on the C oracle: every step equals the reference recording (tests/golden/battle*_rollout), with
+    the episode returns summed in each engine's team orders (k_rollout 64 / 256, the few-env stepper 64 / 512,
+    the large-env queue kernel 512)."""
     import rollout_check as rck
-    fx = rck.RolloutFixture()
+    fx = rck.RolloutFixture(name, lanes)
     c = fx.case
     rep = rck.EnvReplay(c["map_size"], fx.placement, c["env"], c["n_envs"], c["max_steps"], True, c["seed"], c["eps"],
-                        "k_rollout_bigq", lanes=(512, 512))
+                        "k_rollout_bigq", lanes=lanes)
     for t in range(c["steps"]):
         rep.advance(t + 1)
         bad = fx.compare(rck.replay_records(rep), 0, t)

@@ -985,6 +985,63 @@ def test_rollout_few_pipe_matches_queue_step(E, S, monkeypatch):
         assert torch.equal(x, y), k
 
 
+@pytest.mark.parametrize("E,S", [(8, 7), (20, 0), (20, 300)])
+def test_rollout_few_pipe_one_workgroup_per_xcd(E, S, monkeypatch):
+    """Forward progress without co-residency: the pipelined few-env form launched with ONE
+    workgroup per XCD (MFX_BIGQ_GRID=8), as when other work on the device holds every other slot.  Each XCD's single
+    workgroup claims its first env's stepper role, takes back every observation item of its own filings (few_steal)
+    and observes them after its step (few_stolen), then -- once its launch steps are done -- claims the XCD's next env
+    from the ticket wait (bigq_wait's kQClaim; E = 20: two or three envs per XCD) and skips the stolen slots.
+    Against the queue kernel's step-after-items form (MFX_FEW_PIPE=0, full grid): every output buffer and the
+    per-call ids / positions / hp bit for bit after 432 steps (every env restarts)."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    N, T = 128, 432
+    left, right = bd.block_positions(64, N)
+    dumps = []
+    for mode, grid in (("0", None), ("1", "8")):
+        monkeypatch.setenv("MFX_FEW_PIPE", mode)
+        if grid:
+            monkeypatch.setenv("MFX_BIGQ_GRID", grid)
+        eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=97, stagger=True)
+        eng.rollout_substeps(S)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        eng.rollout_step(T)
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, N))
+        del eng
+        monkeypatch.delenv("MFX_BIGQ_GRID", raising=False)
+    for (k, x), (_, y) in zip(dumps[0], dumps[1]):
+        assert torch.equal(x, y), k
+
+
+def test_rollout_bigq_queue_step_one_workgroup_per_xcd(monkeypatch):
+    """The queue kernel's step-after-items form (MFX_FEW_PIPE=0) with one workgroup per XCD (MFX_BIGQ_GRID=8): its
+    waits are only on work held by running workgroups of the same XCD, and a workgroup leaves once its XCD's env-steps
+    of the launch are done (xcd_done), so one resident workgroup per XCD completes the launch.  Against the full
+    grid, bit for bit, 12 staggered 64x64 envs, 20 steps per launch, 432 steps."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    N, T, E = 128, 432, 12
+    left, right = bd.block_positions(64, N)
+    monkeypatch.setenv("MFX_FEW_PIPE", "0")
+    dumps = []
+    for grid in (None, "8"):
+        if grid:
+            monkeypatch.setenv("MFX_BIGQ_GRID", grid)
+        eng = BattleBatch(64, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=31, stagger=True)
+        eng.rollout_substeps(20)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        eng.rollout_step(T)
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, N))
+        del eng
+    for (k, x), (_, y) in zip(dumps[0], dumps[1]):
+        assert torch.equal(x, y), k
+
+
 def test_rollout_substeps_auto_choice():
     """rollout_substeps(0): the engine picks the steps per launch for its path and batch (BattleEngine::sub_steps):
     1024 for the pipelined few-env stepper (in practice the whole rollout_step), 2 for k_rollout below 96 envs per
@@ -1014,9 +1071,9 @@ def test_rollout_substeps_auto_choice():
 @pytest.mark.parametrize("E", [8, 64])
 def test_rollout_two_engines_two_streams(E):
     """Two engines on two streams of one device, both on the pipelined few-env path, their launches enqueued back to
-    back: the queue kernels need their whole persistent grid resident, so the engine serialises them process-wide
-    (BigqSerial) instead of letting two grids share the card -- both finish without a stalled wait (rollout_check)
-    and, seeded alike, leave identical buffers."""
+    back and running at once (the pipelined form is not serialised: it needs one resident workgroup per XCD, and a
+    launch leaves an XCD once its work there is done) -- both finish without a stalled wait (rollout_check) and,
+    seeded alike, leave identical buffers."""
     import torch
     from mfrl_amd.battle import BattleBatch
     N = 128
