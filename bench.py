@@ -306,24 +306,37 @@ def run_check(eng, args, E, placement, seed, world):
     import rollout_check as rc
     steps = args.max_steps + args.warmup + args.steps            # every step since rollout_init
     envs = rc.sample_envs(E, args.check_envs)
+    ref_lib = os.path.join(REPO, "oracle", "_ref", "libmagent_ref.so")
+    ref_env = envs[len(envs) // 2] if os.path.exists(ref_lib) else None
     t = time.perf_counter()
     err = None
+    bad_ref = []
     try:
         chk = rc.RolloutChecker(eng, args.map, placement, envs, args.max_steps, True, seed, 0.2)
         bad = chk.check(steps)
+        if ref_env is not None:
+            # one of the sampled envs replayed on the reference engine itself as well
+            ref = rc.RolloutChecker(eng, args.map, placement, [ref_env], args.max_steps, True, seed, 0.2, lib=ref_lib)
+            bad_ref = ref.check(steps)
     except Exception as x:                  # a device / queue error word (rollout_check) or a failed read
         bad, err = ["%s: %s" % (type(x).__name__, x)], True
+    bad = bad + ["reference build: " + b for b in bad_ref]
     ok = torch.tensor([0.0 if bad else 1.0], dtype=torch.float64, device="cuda")
     n = torch.tensor([float(len(envs))], dtype=torch.float64, device="cuda")
+    nref = torch.tensor([0.0 if ref_env is None else 1.0], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         dist.all_reduce(n)
+        dist.all_reduce(nref)
     return {"ok": bool(ok.item() == 1.0), "envs": int(n.item()), "envs_per_rank": len(envs), "steps": steps,
             "sample_rank0": envs, "path": eng.rollout_path() if err is None else None,
+            "reference_envs": int(nref.item()), "reference_env_rank0": ref_env,
             "what": "each sampled env replayed from rollout_init on the C oracle (oracle/battle_oracle.c) with a "
-                    "host restatement of the device rush policy; last step's views, features, actions, rewards, "
-                    "mean action, post-step ids / positions / hp, agent-steps, episode statistics and return "
-                    "compared bit for bit; device and queue error words read (rollout_check); after the clock",
+                    "host restatement of the device rush policy, and one of them (reference_env_rank0) also on the "
+                    "reference engine itself (oracle/_ref, built from /root/reference); last step's views, features, "
+                    "actions, rewards, mean action, post-step ids / positions (/ hp on the C oracle), agent-steps, "
+                    "episode statistics and return compared bit for bit; device and queue error words read "
+                    "(rollout_check); after the clock",
             "seconds": time.perf_counter() - t, "mismatches": bad[:16]}
 
 
@@ -479,7 +492,9 @@ def main():
     # stream around the whole region (an event pair around every launch put two timestamp packets between
     # consecutive launches: at 8192 envs x 2 steps per launch ~5 % of the wall time went to them)
     chunks = [min(S, args.steps - k) for k in range(0, args.steps, S)]
-    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    # one event pair per run of launches between collectives (one run at world 1): the roofline's kernel time
+    # leaves the statistics' all-reduce and the wait for other ranks out
+    segs = []
     a0 = agent_steps()
     if world > 1:
         dist.barrier()
@@ -487,15 +502,21 @@ def main():
     t0 = time.perf_counter()
     red = None
     done_steps = 0
-    ev[0].record(stream)
     for k, n in enumerate(chunks):
+        if not segs or segs[-1][1] is not None:
+            segs.append([torch.cuda.Event(enable_timing=True), None])
+            segs[-1][0].record(stream)
         eng.rollout_step(n)
         done_steps += n
         # episode statistics -> RCCL all-reduce, once per episode batch (an episode cap of steps) and at
         # the end of the timed window: the only collective
         if world > 1 and (done_steps // args.max_steps != (done_steps - n) // args.max_steps or k == len(chunks) - 1):
+            segs[-1][1] = torch.cuda.Event(enable_timing=True)
+            segs[-1][1].record(stream)
             red = reduce_stats(stats())
-    ev[1].record(stream)
+    if segs[-1][1] is None:
+        segs[-1][1] = torch.cuda.Event(enable_timing=True)
+        segs[-1][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -504,8 +525,9 @@ def main():
     if red is None:                  # one rank: the same statistics, reduced after the clock
         red = reduce_stats(stats())
     red = red.tolist()
-    # the mean launch of the timed region (its launches back to back on the stream: the region / their count)
-    kernel_ms = ev[0].elapsed_time(ev[1]) / len(chunks)
+    # the mean launch of the timed region (its launches back to back on the stream between collectives: the runs'
+    # time / their launch count)
+    kernel_ms = sum(a.elapsed_time(b) for a, b in segs) / len(chunks)
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
     check = run_check(eng, args, E, [left, right], env_seed(1234, rank), world)
@@ -553,8 +575,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kernel_ms,
                          "kernel_ms_is": "mean launch duration: HIP events on the launch stream around the timed "
-                                         "region's %d launch(es), / their count; %g step(s) per launch"
-                                         % (len(chunks), steps_per_timed_launch),
+                                         "region's %d launch(es) (%d run(s) of back-to-back launches between "
+                                         "collectives), / their count; %g step(s) per launch"
+                                         % (len(chunks), len(segs), steps_per_timed_launch),
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch,
                          "grid": grid, "lds_bytes": lds},
             "cpu_baseline": None,

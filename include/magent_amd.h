@@ -2,7 +2,7 @@
  * magent_amd.h -- C ABI of the MI355X-native Battle / Ising mean-field engine (libmagent.so).
  *
  * Part 1 is the reference's own ABI, symbol for symbol: the 18 GridWorld entry points of
- * examples/battle_model/src/runtime_api.h:118-181 (implemented at runtime_api.cc:15-169), so
+ * examples/battle_model/src/runtime_api.h:20-55 (implemented at runtime_api.cc:15-169), so
  * the reference python wrapper examples/battle_model/python/magent/gridworld.py (ctypes, no
  * argtypes) and c_lib.py:13-31 bind this library unchanged.  Those calls act on env 0 and move
  * data through caller-owned host buffers, exactly like the reference.  On one env whose config the
@@ -33,46 +33,46 @@ extern "C" {
 #endif
 
 /* ---------------------------------------------------------------- part 1: reference ABI */
-/* runtime_api.h:118 env_new_game -- name must be "GridWorld" (DiscreteSnake is out of scope) */
+/* runtime_api.h:20 env_new_game -- name must be "GridWorld" (DiscreteSnake is out of scope) */
 int env_new_game(void **game, const char *name);
-/* runtime_api.h:119 */
+/* runtime_api.h:21 */
 int env_delete_game(void *game);
-/* runtime_api.h:120 -- keys of GridWorld::set_config (GridWorld.cc:126-155): map_width,
+/* runtime_api.h:22 -- keys of GridWorld::set_config (GridWorld.cc:126-155): map_width,
  * map_height (int*), minimap_mode, food_mode, turn_mode, goal_mode (bool*), embedding_size (int*),
  * render_dir (char*), seed (int*) -- every key the reference accepts */
 int env_config_game(void *game, const char *key, void *value);
-/* runtime_api.h:123 */
+/* runtime_api.h:25 */
 int env_reset(void *game);
-/* runtime_api.h:124 -- bufs[0] = float[n][view_h][view_w][n_ch], bufs[1] = float[n][feature] */
+/* runtime_api.h:26 -- bufs[0] = float[n][view_h][view_w][n_ch], bufs[1] = float[n][feature] */
 int env_get_observation(void *game, int group, float **bufs);
-/* runtime_api.h:125 -- actions int32[n] in group-vector order */
+/* runtime_api.h:27 -- actions int32[n] in group-vector order */
 int env_set_action(void *game, int group, const int *actions);
-/* runtime_api.h:126 */
+/* runtime_api.h:28 */
 int env_step(void *game, int *done);
-/* runtime_api.h:127 -- float[n] */
+/* runtime_api.h:29 -- float[n] */
 int env_get_reward(void *game, int group, float *buffer);
-/* runtime_api.h:130 -- num, id, pos, alive, action_space, view_space, feature_space,
+/* runtime_api.h:32 -- num, id, pos, alive, action_space, view_space, feature_space,
  * view2attack, attack_base, both_attack, global_minimap, mean_info, walls_info,
  * render_window_info, attack_event, groups_info (GridWorld.cc:777-978) */
 int env_get_info(void *game, int group, const char *name, void *buffer);
-/* runtime_api.h:133-134 -- RenderGenerator's frame files: config.json + video_<n>.txt of env 0
+/* runtime_api.h:35-36 -- RenderGenerator's frame files: config.json + video_<n>.txt of env 0
  * (RenderGenerator.cc), byte-identical to the reference build's; only the websocket server and the
  * JS viewer are out of scope */
 int env_render(void *game);
 int env_render_next_file(void *game);
-/* runtime_api.h:140 -- AgentType reflection keys (AgentType.cc:63-101) */
+/* runtime_api.h:42 -- AgentType reflection keys (AgentType.cc:63-101) */
 int gridworld_register_agent_type(void *game, const char *name, int n, const char **keys, float *values);
-/* runtime_api.h:141 */
+/* runtime_api.h:43 */
 int gridworld_new_group(void *game, const char *agent_type_name, int *group);
-/* runtime_api.h:142-143 -- method "custom" | "random" | "fill"; group -1 = walls */
+/* runtime_api.h:44-45 -- method "custom" | "random" | "fill"; group -1 = walls */
 int gridworld_add_agents(void *game, int group, int n, const char *method, const int *pos_x, const int *pos_y,
                          const int *dir);
-/* runtime_api.h:146 */
+/* runtime_api.h:48 */
 int gridworld_clear_dead(void *game);
-/* runtime_api.h:147 -- "random" only (GridWorld.cc:729-740): advances the engine LCG like the
+/* runtime_api.h:49 -- "random" only (GridWorld.cc:729-740): advances the engine LCG like the
  * reference, goals are never read back */
 int gridworld_set_goal(void *game, int group, const char *method, const int *linear_buffer);
-/* runtime_api.h:150-153 -- the full reward DSL (RewardEngine.cc:14-443): and / or / not over
+/* runtime_api.h:52-55 -- the full reward DSL (RewardEngine.cc:14-443): and / or / not over
  * attack / kill / collide / at / in / die / in_a_line events, 'any' / 'all' / fixed-index symbols,
  * group receivers, terminal rules.  Rules of the one-event attack/kill/collide form run
  * data-parallel, the rest through a one-lane interpreter; 'align' fails loudly (the reference
@@ -82,13 +82,13 @@ int gridworld_define_agent_symbol(void *game, int no, int group, int index);
 int gridworld_define_event_node(void *game, int no, int op, int *inputs, int n_inputs);
 int gridworld_add_reward_rule(void *game, int on, int *receiver, float *value, int n_receiver, bool is_terminal,
                               bool auto_value);
-/* Extension of env_get_observation (runtime_api.h:124) for the drop-in python: the same views and
+/* Extension of env_get_observation (runtime_api.h:26) for the drop-in python: the same views and
  * features of env 0 (n agents), as pointers into engine-owned pinned memory the drop-in step wrote
  * them to (no copy), in blocks of `rows` agents that stay at those addresses until the group
  * outgrows them; valid until the step after next or env_delete_game.  Returns 1 (nothing set) when
  * the observation is not held that way -- call env_get_observation then. */
 int mfx_env_observation_view(void *game, int group, float **view, float **feature, int *n, int *rows);
-/* Extension of env_get_info("num") + env_get_info("id" / "alive" / "pos") / env_get_reward (runtime_api.h:125-127)
+/* Extension of env_get_info("num") + env_get_info("id" / "alive" / "pos") / env_get_reward (runtime_api.h:29, :32)
  * for the drop-in python: one call per getter.  Returns the group's agent count n and, when n <= cap, copies
  * its n rows of field `what` (0 id int32, 1 reward float32, 2 alive uint8, 3 pos int32 x 2; -1: the count only)
  * into out; -1 on error. */
@@ -220,8 +220,9 @@ int mfx_acnet_act_rollout(void *handle, const float *d_view, const float *d_feat
 /* The data path of the replay buffers (algo/tools.py:26-362): for i < n, row idx[i] (or i; modulo src_mod
  * when > 0) of every source column -> row dst_start + i (modulo dst_cap when > 0) of its destination column;
  * n_cols <= 8, row_bytes per column; one launch (csrc/replay_kernels.hip).  src_rows: rows of every source
- * column -- a source index outside it (the reference's numpy indexing raises IndexError) skips the row and is
- * reported by mfx_rows_copy_error (synchronising; -1 and *bad_index when one was met, then cleared). */
+ * column -- without src_mod an index in [-src_rows, 0) counts from the end, as numpy's indexing does; any other
+ * index outside [0, src_rows) (the reference's numpy indexing raises IndexError) skips the row and is reported by
+ * mfx_rows_copy_error (synchronising; -1 and *bad_index when one was met, -1 included, then cleared). */
 int mfx_rows_copy(int n_cols, void *const *dst, const void *const *src, const int64_t *row_bytes, const int64_t *d_idx,
                   int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap, int64_t n, void *stream);
 int mfx_rows_copy_error(int64_t *bad_index, void *stream);

@@ -1560,6 +1560,9 @@ public:
     // heaviest units end the launch: 8192 envs 0.556 -> 0.594 of peak, 16384 0.62 -> 0.63), else 20 (32768
     // envs 0.75 at 5, 0.77 at 20; the bench's 131072, 0.84-0.86); the large-env queue kernel 20.
     int sub_steps() const {
+        // (one step per launch: the two-kernel observation / step pipeline and the large-env two-stream pipeline --
+        // rollout_step launches those per step whatever ro_sub says)
+        if (ro_pipe || (ro_big && !ro_bigq)) return 1;
         const bool pipe = ro_big && ro_bigq && ra.few_pipe;
         if (ro_sub > 0) return std::min(ro_sub, pipe ? kMaxPipeSub : kMaxSub);
         if (ro_big) return pipe ? kMaxPipeSub : 20;

@@ -67,9 +67,24 @@ __device__ __forceinline__ void row_copy16(const uint4* __restrict__ sp, uint4* 
     }
 }
 
-// First out-of-range source index seen by k_rows_copy, plus one (0: none); read and cleared by
-// mfx_rows_copy_error.  A bad row is skipped, never read.
-__device__ unsigned long long g_rows_bad;
+// The first out-of-range source index the row movers met: the workgroup whose compare-and-swap sets the flag
+// stores the index (any int64, -1 included); read and cleared by mfx_rows_copy_error.  A bad row is skipped,
+// never read.
+__device__ unsigned int g_rows_bad_flag;
+__device__ long long g_rows_bad_index;
+
+__device__ __forceinline__ void rows_bad(int64_t raw) {
+    if (atomicCAS(&g_rows_bad_flag, 0u, 1u) == 0u) g_rows_bad_index = (long long)raw;
+}
+
+// The source row of index raw: modulo src_mod when > 0 (the rings), else numpy's indexing of src_rows rows
+// (-src_rows..-1 count from the end); -1 when out of range.
+__device__ __forceinline__ int64_t rows_src(int64_t raw, int64_t src_mod, int64_t src_rows) {
+    int64_t s = raw;
+    if (src_mod > 0) { s %= src_mod; if (s < 0) s += src_mod; }
+    else if (s < 0) s += src_rows;
+    return (s < 0 || s >= src_rows) ? -1 : s;
+}
 
 // One wave per row (four rows per workgroup): row s = idx ? idx[i] : i (modulo src_mod) of every column to
 // row d = dst_start + i (modulo dst_cap).  The narrow columns in one pass of unit loads, then each wide
@@ -80,10 +95,10 @@ __global__ void __launch_bounds__(256) k_rows_copy(RowCols c, const int64_t* __r
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * 4;
     for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += waves) {
-        int64_t s = idx ? idx[i] : i;
-        if (src_mod > 0) { s %= src_mod; if (s < 0) s += src_mod; }
-        if (s < 0 || s >= src_rows) {
-            if (lane == 0) atomicCAS(&g_rows_bad, 0ull, (unsigned long long)(idx ? idx[i] : i) + 1ull);
+        const int64_t raw = idx ? idx[i] : i;
+        const int64_t s = rows_src(raw, src_mod, src_rows);
+        if (s < 0) {
+            if (lane == 0) rows_bad(raw);
             continue;
         }
         int64_t d = dst_start + i;
@@ -146,11 +161,10 @@ __global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wd
     auto locate = [&](int64_t i, PipeRow& r) {
         r.ok = i < n;
         if (!r.ok) return;
-        int64_t s = idx ? idx[i] : i;                      // wave-uniform: a scalar load
-        const int64_t raw = s;
-        if (src_mod > 0) { s %= src_mod; if (s < 0) s += src_mod; }
-        if (s < 0 || s >= src_rows) {
-            if (lane == 0) atomicCAS(&g_rows_bad, 0ull, (unsigned long long)raw + 1ull);
+        const int64_t raw = idx ? idx[i] : i;              // wave-uniform: a scalar load
+        const int64_t s = rows_src(raw, src_mod, src_rows);
+        if (s < 0) {
+            if (lane == 0) rows_bad(raw);
             r.ok = false;
             return;
         }
@@ -232,11 +246,10 @@ __global__ void __launch_bounds__(256) k_rows_batch(RowCols c, int wk, int64_t w
             const int64_t i = i0 + k * W;
             r[k].ok = i < n;
             if (!r[k].ok) continue;
-            int64_t sidx = idx ? idx[i] : i;
-            const int64_t raw = sidx;
-            if (src_mod > 0) { sidx %= src_mod; if (sidx < 0) sidx += src_mod; }
-            if (sidx < 0 || sidx >= src_rows) {
-                if (lane == 0) atomicCAS(&g_rows_bad, 0ull, (unsigned long long)raw + 1ull);
+            const int64_t raw = idx ? idx[i] : i;
+            const int64_t sidx = rows_src(raw, src_mod, src_rows);
+            if (sidx < 0) {
+                if (lane == 0) rows_bad(raw);
                 r[k].ok = false;
                 continue;
             }
@@ -294,8 +307,8 @@ extern "C" {
 // to row d = dst_start + i (modulo dst_cap when dst_cap > 0) of the destination column.  n_cols <= 8;
 // row_bytes[k]: bytes per row of column k.  Destination rows of one call must be distinct (a ring shorter
 // than n would make two rows race for a slot: the caller skips the rows a ring would overwrite).
-// src_rows: rows every source column holds; an index outside [0, src_rows) (after the modulo) skips its row and
-// is reported by mfx_rows_copy_error.
+// src_rows: rows every source column holds; without src_mod an index in [-src_rows, 0) counts from the end (numpy's
+// indexing); any other index outside [0, src_rows) skips its row and is reported by mfx_rows_copy_error.
 MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, const int64_t* row_bytes,
                           const int64_t* d_idx, int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap,
                           int64_t n, void* stream) {
@@ -369,13 +382,16 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
 // Synchronises `stream`; *bad_index = the first out-of-range source index any k_rows_copy met since the last
 // call (-1: none), and the word is cleared.  Returns -1 (with the message) when one was met.
 MFX_API int mfx_rows_copy_error(int64_t* bad_index, void* stream) {
-    unsigned long long h = 0;
+    unsigned int flag = 0;
+    long long h = -1;
     MFX_HIP(hipStreamSynchronize((hipStream_t)stream));
-    MFX_HIP(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_rows_bad), sizeof(h), 0, hipMemcpyDeviceToHost));
-    *bad_index = h ? (int64_t)(h - 1ull) : -1;
-    if (!h) return 0;
-    const unsigned long long z = 0;
-    MFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rows_bad), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+    MFX_HIP(hipMemcpyFromSymbol(&flag, HIP_SYMBOL(g_rows_bad_flag), sizeof(flag), 0, hipMemcpyDeviceToHost));
+    *bad_index = -1;
+    if (!flag) return 0;
+    MFX_HIP(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_rows_bad_index), sizeof(h), 0, hipMemcpyDeviceToHost));
+    *bad_index = (int64_t)h;
+    const unsigned int z = 0;
+    MFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rows_bad_flag), &z, sizeof(z), 0, hipMemcpyHostToDevice));
     return fail("rows_copy: source index %lld out of range (row skipped)", (long long)*bad_index);
 }
 

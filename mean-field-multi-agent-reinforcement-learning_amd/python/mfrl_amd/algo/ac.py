@@ -43,9 +43,10 @@ class ActorCritic:
         self._hip = None
         self._hip_key = None
         self._draws = 0             # act() calls: the step counter of the device draw
-        # the draw's seed: fixed per model name (np.random is left alone -- the reference consumes it in the
-        # replay buffers, and seeded runs must draw the same indices)
-        self.seed = zlib.crc32(("%s/%s" % (self._prefix, name)).encode())
+        # the draw's seed: the run's torch seed mixed with the model name, so runs seeded alike draw alike and
+        # differently seeded runs differ, as tf.multinomial under TF's seed would; np.random is left
+        # alone -- the reference consumes it in the replay buffers, and seeded runs must draw the same indices
+        self.seed = zlib.crc32(("%s/%s/%d" % (self._prefix, name, torch.initial_seed())).encode())
 
     @property
     def vars(self):

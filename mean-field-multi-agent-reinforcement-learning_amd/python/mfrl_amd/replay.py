@@ -14,9 +14,10 @@ _MAX_COLS = 8
 def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
     """For i < n: row (idx[i] if idx is not None else i), taken modulo src_mod if > 0, of every tensor in
     `src` -> row dst_start + i (modulo dst_cap if > 0) of the matching tensor in `dst`.  Tensors: CUDA,
-    contiguous, first dimension = rows, equal row byte sizes pairwise.  A source index outside the source
-    rows is skipped on the device and raised by the next check_errors() (the reference's numpy indexing raises
-    IndexError at once; checking here would synchronise every move)."""
+    contiguous, first dimension = rows, equal row byte sizes pairwise.  Without src_mod, an index in
+    [-rows, 0) counts from the end as numpy's does; any other index outside the source rows is skipped on the
+    device and raised by the next check_errors() (the reference's numpy indexing raises IndexError at once;
+    checking here would synchronise every move)."""
     assert len(dst) == len(src) and 0 < len(dst) <= _MAX_COLS
     if n is None:
         n = len(idx) if idx is not None else src[0].shape[0]

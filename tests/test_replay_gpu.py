@@ -67,3 +67,16 @@ def test_rows_copy_out_of_range_index_raises():
     for a, x in zip(dst, src):
         assert torch.equal(a[0], x[5]) and torch.equal(a[2], x[7])
         assert not a[1].any() and not a[3].any()
+    # numpy's negative indices count from the end (-64 is row 0, -1 row 63); -65 is out of range and is reported
+    # as itself (the bad-index word once stored index + 1, so -1 read as 'none')
+    for a in dst:
+        a.zero_()
+    rows_copy(dst, src, torch.tensor([-1, -64, -65, 3], dtype=torch.int64, device="cuda"))
+    with pytest.raises(IndexError, match="index -65 out of range"):
+        check_errors()
+    for a, x in zip(dst, src):
+        assert torch.equal(a[0], x[63]) and torch.equal(a[1], x[0]) and torch.equal(a[3], x[3])
+        assert not a[2].any()
+    rows_copy(dst, src, torch.tensor([2, -100], dtype=torch.int64, device="cuda"), n=2)
+    with pytest.raises(IndexError, match="index -100 out of range"):
+        check_errors()

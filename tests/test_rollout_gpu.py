@@ -400,6 +400,35 @@ def test_rollout_bigq_matches_reference_recording(E, S):
     assert fx.restart.sum() == 2
 
 
+@pytest.mark.parametrize("E,S,path", [(131072, 20, "k_rollout"), (8, 0, "k_rollout_bigq"), (1, 1, "k_rollout_bigq")])
+def test_rollout_matches_reference_recording_64(E, S, path):
+    """The headline kernel against the REFERENCE engine's own recording (tests/golden/battle64_rollout.npz,
+    make_battle_fixtures.py): env 0 of the 64x64 bench batch (128 + 128 agents, device rush policy,
+    seed 1234) through two full 400-step episodes.  (131072, 20): k_rollout at the bench's batch and launch shape,
+    compared at every launch boundary; (8, 0): configs[3]'s per-GPU batch on the pipelined few-env stepper with the
+    engine's steps per launch, compared every 20 steps; (1, 1): one env, after every step.  The episode returns
+    follow the engine's own reward-sum teams (rollout_sum_lanes), which the recording holds in every order."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    c = common.manifest()["cases"]["battle64_rollout"]
+    eng = BattleBatch(c["map_size"], E, stream=torch.cuda.current_stream())
+    left, right = bd.block_positions(64, 128)
+    eng.rollout_init([left, right], max_steps=c["max_steps"], eps=c["eps"], seed=c["seed"], stagger=True)
+    eng.rollout_substeps(S)
+    assert eng.rollout_path() == path, eng.rollout_path()
+    fx = rck.RolloutFixture("battle64_rollout", (eng.rollout_sum_lanes(64), eng.rollout_sum_lanes(65)))
+    K = S if S > 0 else 20
+    t = 0
+    while t < c["steps"]:
+        k = min(K, c["steps"] - t)
+        eng.rollout_step(k)
+        t += k
+        eng.rollout_check()
+        bad = fx.compare(rck.device_records(eng, [0]), 0, t - 1)
+        assert not bad, bad[:8]
+    assert fx.restart.sum() == 2
+
+
 def test_rollout_bigq_bench_shape_matches_reference_build():
     """The 256x256 bench batch (2048 staggered envs, 20 steps per launch, 420 steps) with 4 sampled envs
     replayed on the reference engine itself (oracle/_ref, one thread) instead of the C oracle."""
