@@ -163,6 +163,13 @@ int mfx_ising_step(void *handle, const int32_t *actions, double *reward, uint8_t
 int mfx_ising_mfq_run(void *handle, int T, double temperature, double lr, double decay_rate, int decay_gap,
                       const double *u, const uint32_t *mask, unsigned seed, double *q, double *order,
                       int32_t *n_up, int32_t *steps);
+/* main_MFQ_Ising.py with its numpy RandomState stream generated on the device (MT19937, numpy's legacy draws: the
+ * Boltzmann uniforms and the act_group permutation): replica r runs the script with seed seed0 + r for `episodes`
+ * episodes in sequence on one stream (-epi), each until its early stop; outputs per episode (host, nullable except
+ * q): q [E][R][N][K+1][2], order [E][R][T], n_up [E][R][T], steps [E][R]. */
+int mfx_ising_mfq_run_stream(void *handle, int T, double temperature, double lr, double decay_rate, int decay_gap,
+                             double act_rate, unsigned seed0, int episodes, double *q, double *order, int32_t *n_up,
+                             int32_t *steps);
 
 /* ---------------------------------------------------------------- part 4: mean-field kernels */
 /* senario_battle.py:141 */

@@ -5,6 +5,7 @@
 // package and `mfrl_amd.ising` bind through ctypes; host buffers in, host buffers out.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -23,6 +24,9 @@ struct IsingEngine {
     DevBuf<double> reward, order, q, u, order_t;
     DevBuf<uint32_t> mask;
     DevBuf<int32_t> nup_t;
+    DevBuf<uint32_t> words, off[2];          // the device stream (mfx_ising_mfq_run_stream)
+    DevBuf<uint16_t> perm;
+    DevBuf<int32_t> err;
     ~IsingEngine() { if (stream) (void)hipStreamDestroy(stream); }
 };
 
@@ -130,6 +134,87 @@ MFX_API int mfx_ising_mfq_run(void* h, int T, double temperature, double lr, dou
     if (n_up) MFX_HIP(hipMemcpyAsync(n_up, e->nup_t.p, sizeof(int32_t) * R * T, hipMemcpyDeviceToHost, e->stream));
     if (steps) MFX_HIP(hipMemcpyAsync(steps, e->steps.p, sizeof(int32_t) * R, hipMemcpyDeviceToHost, e->stream));
     MFX_HIP(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// main_MFQ_Ising.py with its numpy stream generated on the device (k_mt_words, k_ising_scan): replica r is the
+// script run with seed seed0 + r -- RandomState(seed0 + r), make_world's N discarded choice(2) draws, then per
+// episode env.reset's N spins and per step the N Boltzmann uniforms and the act_group permutation
+// (choice(N, int(act_rate N), replace=False)) -- for `episodes` episodes in sequence on the one stream, each until
+// its own early stop (-epi).  Nothing is read back between episodes: the next episode's first draw is found on the
+// device from the steps the previous one ran.  Outputs (host; nullable except q), per episode:
+// q [E][R][N][K+1][2], order [E][R][T], n_up [E][R][T], steps [E][R]; the spins end as the last episode left them.
+MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double lr, double decay_rate, int decay_gap,
+                                     double act_rate, unsigned seed0, int episodes, double* q, double* order,
+                                     int32_t* n_up, int32_t* steps) {
+    auto* e = static_cast<IsingEngine*>(h);
+    const int R = e->R, N = e->N, K = e->K, mw = (N + 31) / 32;
+    if (T < 1 || episodes < 1) return mfx::fail("ising mfq stream: T and episodes must be >= 1");
+    if (decay_gap < 1) return mfx::fail("ising mfq stream: decay_gap must be >= 1");
+    if (!(act_rate >= 0.0 && act_rate <= 1.0)) return mfx::fail("ising mfq stream: act_rate must be in [0, 1]");
+    const int n_upd = (int)(act_rate * N);                  // int(act_rate * n_agents), main_MFQ_Ising.py:126
+    // words per replica: make_world's N, then per episode N spins and per step 2 N uniforms + the permutation's
+    // draws (N - 1 accepted words plus rejections: ~0.5 N expected, bounded here by 2 N -- a walk past the end sets
+    // the error word) + one chunk of read-ahead
+    const size_t per = (size_t)N + (size_t)episodes * ((size_t)N + (size_t)T * 4 * N) + 64;
+    const int blocks = (int)((per + 623) / 624);
+    const size_t W = (size_t)blocks * 624;
+    // replicas per pass: the word streams within ~16 GB
+    const int Rb = (int)std::max<size_t>(1, std::min<size_t>((size_t)R, ((size_t)16 << 30) / (W * 4)));
+    const size_t QR = (size_t)N * (K + 1) * 2;
+    try {
+        e->words.ensure((size_t)Rb * W);
+        for (auto& o : e->off) o.ensure((size_t)Rb * (T + 1));
+        e->err.ensure(1);
+        if (n_upd < N) { e->perm.ensure((size_t)Rb * N); e->mask.ensure((size_t)Rb * T * mw); }
+        e->q.ensure((size_t)Rb * QR);
+        e->order_t.ensure((size_t)Rb * T);
+        e->nup_t.ensure((size_t)Rb * T);
+        e->steps.ensure(Rb);
+        e->spins_out.ensure((size_t)R * N);
+    } catch (const std::exception& ex) {
+        return mfx::fail("%s", ex.what());
+    }
+    MFX_HIP(hipMemsetAsync(e->err.p, 0, sizeof(int32_t), e->stream));
+    for (int r0 = 0; r0 < R; r0 += Rb) {
+        const int nr = std::min(Rb, R - r0);
+        MFX_HIP(mfx::launch_mt_words(seed0, r0, nr, blocks, e->words.p, W, e->stream));
+        for (int ep = 0; ep < episodes; ++ep) {
+            mfx::IsingScanArgs sa{};
+            sa.N = N; sa.T = T; sa.n_upd = n_upd; sa.words = e->words.p; sa.wstride = W;
+            sa.prev_off = ep ? e->off[(ep - 1) & 1].p : nullptr;
+            sa.prev_steps = ep ? e->steps.p : nullptr;
+            sa.spins0 = e->spins.p + (size_t)r0 * N;
+            sa.off = e->off[ep & 1].p;
+            sa.mask = n_upd < N ? e->mask.p : nullptr;
+            sa.perm = n_upd < N ? e->perm.p : nullptr;
+            sa.err = e->err.p;
+            MFX_HIP(mfx::launch_ising_scan(sa, nr, e->stream));
+            mfx::IsingMfqArgs a{};
+            a.N = N; a.K = K; a.T = T; a.nbr = e->nbr.p; a.spins0 = e->spins.p + (size_t)r0 * N;
+            a.words = e->words.p; a.woff = e->off[ep & 1].p; a.wstride = W;
+            a.mask = n_upd < N ? e->mask.p : nullptr;
+            a.temperature = temperature; a.lr = lr; a.decay_rate = decay_rate; a.decay_gap = decay_gap;
+            a.q_out = e->q.p; a.order_out = e->order_t.p; a.nup_out = e->nup_t.p;
+            a.spins_out = e->spins_out.p + (size_t)r0 * N; a.steps_out = e->steps.p;
+            MFX_HIP(mfx::launch_ising_mfq(a, nr, e->stream));
+            const size_t er = (size_t)ep * R + r0;               // this pass's rows of episode ep's outputs
+            MFX_HIP(hipMemcpyAsync(q + er * QR, e->q.p, sizeof(double) * nr * QR, hipMemcpyDeviceToHost, e->stream));
+            if (order)
+                MFX_HIP(hipMemcpyAsync(order + er * T, e->order_t.p, sizeof(double) * nr * T, hipMemcpyDeviceToHost,
+                                       e->stream));
+            if (n_up)
+                MFX_HIP(hipMemcpyAsync(n_up + er * T, e->nup_t.p, sizeof(int32_t) * nr * T, hipMemcpyDeviceToHost,
+                                       e->stream));
+            if (steps)
+                MFX_HIP(hipMemcpyAsync(steps + er, e->steps.p, sizeof(int32_t) * nr, hipMemcpyDeviceToHost, e->stream));
+        }
+    }
+    MFX_HIP(hipMemcpyAsync(e->spins.p, e->spins_out.p, (size_t)R * N, hipMemcpyDeviceToDevice, e->stream));
+    int32_t err = 0;
+    MFX_HIP(hipMemcpyAsync(&err, e->err.p, sizeof(err), hipMemcpyDeviceToHost, e->stream));
+    MFX_HIP(hipStreamSynchronize(e->stream));
+    if (err) return mfx::fail("ising mfq stream: a replica's draws ran past its %zu generated words", W);
     return 0;
 }
 

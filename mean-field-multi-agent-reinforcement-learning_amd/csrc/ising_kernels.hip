@@ -82,10 +82,181 @@ __device__ __forceinline__ double philox_uniform(uint32_t seed, uint32_t rep, ui
     return (double)bits * (1.0 / 9007199254740992.0);
 }
 
+// ------------------------------------------------------------------ numpy's legacy MT19937 stream
+// main_MFQ_Ising.py draws from numpy's legacy RandomState (numpy/random/mtrand.pyx over
+// numpy/random/src/mt19937): RandomState(seed) = init_genrand(seed) (key[0] = seed, key[i] = 1812433253 *
+// (key[i-1] ^ key[i-1] >> 30) + i), 624-word twists, tempered outputs.  Its consumption, pinned against numpy itself
+// (tests/test_ising_cpu.py test_numpy_stream_model): random_sample = one double from two words (a >> 5, b >> 6);
+// choice(2) = one word & 1 (a masked bounded draw of 1); choice(N, k, replace=False) = permutation(N)[:k], the
+// legacy shuffle of arange(N): for i = N-1 .. 1, j = random_interval(i) -- one word per try, masked to the smallest
+// 2^b - 1 >= i, retried while above i -- then swap(x[i], x[j]).
+constexpr int kMtN = 624;
+__device__ __forceinline__ uint32_t mt_next(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7FFFFFFFu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9D2C5680u;
+    y ^= (y << 15) & 0xEFC60000u;
+    y ^= y >> 18;
+    return y;
+}
+// random_sample's double from words p[0], p[1] (legacy random_standard_uniform / rk_double)
+__device__ __forceinline__ double mt_uniform(const uint32_t* p) {
+    const uint32_t a = p[0] >> 5, b = p[1] >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// One wave per replica, four replicas per workgroup: the state in LDS.  A twist in three passes whose reads all
+// precede their writes: i < 227 reads key[i + 1], key[i + 397] as they were; 227 <= i < 454 reads key[i - 227] of the
+// first pass; the rest reads key[i - 227] of the second and, for i = 623, key[0] of the first.  Each block of 624
+// words is tempered and stored in order: words[r][624 b ...] is the replica's stream from its first draw.
+__global__ void __launch_bounds__(256) k_mt_words(uint32_t seed0, int r0, int R, int n_blocks, uint32_t* __restrict__ words,
+                                                  size_t stride) {
+    __shared__ uint32_t st[4][kMtN];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + wv;
+    if (r >= R) return;                       // (a whole wave: no workgroup barrier below)
+    uint32_t* mt = st[wv];
+    if (lane == 0) {
+        uint32_t x = seed0 + (uint32_t)(r0 + r);
+        mt[0] = x;
+        for (int i = 1; i < kMtN; ++i) {
+            x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+            mt[i] = x;
+        }
+    }
+    wave_lds_fence();
+    uint32_t* out = words + (size_t)r * stride;
+    for (int b = 0; b < n_blocks; ++b) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = lane + 64 * k;
+            if (i < 227) v[k] = mt_next(mt[i], mt[i + 1], mt[i + 397]);
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = lane + 64 * k;
+            if (i < 227) mt[i] = v[k];
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = 227 + lane + 64 * k;
+            if (i < 454) v[k] = mt_next(mt[i], mt[i + 1], mt[i - 227]);
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = 227 + lane + 64 * k;
+            if (i < 454) mt[i] = v[k];
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int i = 454 + lane + 64 * k;
+            if (i < kMtN) v[k] = mt_next(mt[i], mt[i == kMtN - 1 ? 0 : i + 1], mt[i - 227]);
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int i = 454 + lane + 64 * k;
+            if (i < kMtN) mt[i] = v[k];
+        }
+        wave_lds_fence();
+        for (int i = lane; i < kMtN; i += 64) out[(size_t)b * kMtN + i] = mt_temper(mt[i]);
+    }
+}
+
+// One wave per replica: one episode of main_MFQ_Ising.py's draws over the replica's word stream -- env.reset's N
+// spins (choice(2)), then per step the offset of its N uniforms (2 N words) and the act_group permutation's words.
+// The permutation's draws are walked 64 words at a time: lane j holds word j of the chunk; a_j, the draws accepted
+// before it, is the fixed point of a_j = #{l < j : word l accepted when it serves draw m - a_l} (a ballot and a
+// lane count per pass, from the guess a_j = j).  The recursion is triangular -- a_j depends on lanes below j -- so
+// the fixed point is unique and pass k fixes lane k at the latest; a word's decision changes only when its
+// threshold falls between two guesses, so in practice a chunk settles in a few passes.  The chunk ends at the lane
+// that accepts draw 1.  n_upd < N (act_rate < 1): lane 0 also applies the swaps to arange(N) in perm and the first
+// n_upd entries set the step's act_group bits.
+__global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    const uint32_t* W = a.words + (size_t)r * a.wstride;
+    const size_t cap = a.wstride;
+    const int N = a.N, T = a.T, mw = (N + 31) >> 5;
+    const bool perm = a.n_upd < N;
+    uint16_t* x = perm ? a.perm + (size_t)r * N : nullptr;
+    uint32_t* off = a.off + (size_t)r * (T + 1);
+    bool over = false;
+    auto word = [&](size_t p) -> uint32_t {
+        if (p >= cap) { over = true; return 0u; }
+        return W[p];
+    };
+    // the episode's first draw: after make_world's N choice(2) draws, or where the previous episode stopped
+    size_t pos = a.prev_off ? a.prev_off[(size_t)r * (T + 1) + a.prev_steps[r]] : (size_t)N;
+    for (int i = lane; i < N; i += 64) a.spins0[(size_t)r * N + i] = (uint8_t)(word(pos + i) & 1u);
+    pos += N;
+    for (int t = 0; t < T; ++t) {
+        if (lane == 0) off[t] = (uint32_t)pos;
+        pos += 2 * (size_t)N;                                 // the Boltzmann uniforms (k_ising_mfq reads them)
+        if (perm && lane == 0)
+            for (int i = 0; i < N; ++i) x[i] = (uint16_t)i;
+        int m = N - 1;                                       // random_interval(m), m = N-1 .. 1
+        while (m >= 1) {
+            const uint32_t w = word(pos + lane);
+            int acc = 0, aj = lane;
+            unsigned long long bal = 0;
+            for (int it = 0; it <= 64; ++it) {
+                const int mm = m - aj;
+                const uint32_t M = mm >= 1 ? (0xFFFFFFFFu >> __builtin_clz((uint32_t)mm)) : 0u;
+                acc = (mm < 1 || (w & M) <= (uint32_t)mm) ? 1 : 0;
+                bal = __ballot(acc);
+                const int an = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                const bool settled = __ballot(an != aj) == 0ull;
+                aj = an;
+                if (settled) break;
+            }
+            const unsigned long long fin = __ballot(aj + acc >= m);   // the lane accepting draw 1, and after
+            const int used = fin ? __builtin_ctzll(fin) + 1 : 64;
+            if (perm) {                                      // the swaps in draw order (lane 0, one by one)
+                const int mm = m - aj;
+                const uint32_t jv = mm >= 1 ? (w & (0xFFFFFFFFu >> __builtin_clz((uint32_t)mm))) : 0u;
+                for (int l = 0; l < used; ++l) {
+                    const int al = __shfl(acc, l), ml = __shfl(mm, l);
+                    const int jl = (int)__shfl((int)jv, l);
+                    if (lane == 0 && al && ml >= 1) {
+                        const uint16_t xi = x[ml], xj = x[jl];
+                        x[ml] = xj;
+                        x[jl] = xi;
+                    }
+                }
+            }
+            pos += used;
+            m = fin ? 0 : m - __popcll(bal);
+        }
+        if (perm) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            uint32_t* mk = a.mask + ((size_t)r * T + t) * mw;
+            for (int i = lane; i < mw; i += 64) mk[i] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            for (int p = lane; p < a.n_upd; p += 64) {
+                const int v = x[p];
+                atomicOr(&mk[v >> 5], 1u << (v & 31));
+            }
+        }
+    }
+    if (lane == 0) off[T] = (uint32_t)pos;
+    if (__ballot(over) && lane == 0) atomicExch(a.err, 1);
+}
+
 // ------------------------------------------------------------------ fused MF-Q episode
 // One workgroup = one replica = one run of main_MFQ_Ising.py's episode loop.  Thread i owns agent
-// i's Q rows in registers.  u: [T][N] uniforms per replica step (host-generated from numpy's
-// RandomState for bit parity, or null = Philox); mask: [T][ceil(N/32)] act_group bits (null = all).
+// i's Q rows in registers.  The uniforms: numpy's stream generated on the device (words at woff[t] + 2 i:
+// k_mt_words, k_ising_scan), host-uploaded u [T][N], or null = Philox; mask: [T][ceil(N/32)] act_group bits
+// (null = all).
 template <int KMAX>
 __global__ void __launch_bounds__(1024) k_ising_mfq(IsingMfqArgs a) {
     __shared__ uint8_t sp[4096];
@@ -118,7 +289,8 @@ __global__ void __launch_bounds__(1024) k_ising_mfq(IsingMfqArgs a) {
             const double denom = e0 + e1;
             const double p0 = e0 / denom, p1 = e1 / denom;
             const double c0 = p0 / (p0 + p1);                          // cdf /= cdf[-1]
-            const double u = a.u ? a.u[((size_t)r * a.T + t) * N + i]
+            const double u = a.words ? mt_uniform(a.words + (size_t)r * a.wstride + a.woff[(size_t)r * (a.T + 1) + t] + 2 * i)
+                           : a.u ? a.u[((size_t)r * a.T + t) * N + i]
                                  : philox_uniform(a.seed, (uint32_t)r, (uint32_t)t, (uint32_t)i);
             act = (u >= c0) ? 1 : 0;                                   // searchsorted(side='right')
         }
@@ -203,7 +375,8 @@ __global__ void __launch_bounds__(1024) k_ising_mfq_big(IsingMfqArgs a) {
             const double denom = e0 + e1;
             const double p0 = e0 / denom, p1 = e1 / denom;
             const double c0 = p0 / (p0 + p1);
-            const double u = a.u ? a.u[((size_t)r * a.T + t) * N + i]
+            const double u = a.words ? mt_uniform(a.words + (size_t)r * a.wstride + a.woff[(size_t)r * (a.T + 1) + t] + 2 * i)
+                           : a.u ? a.u[((size_t)r * a.T + t) * N + i]
                                  : philox_uniform(a.seed, (uint32_t)r, (uint32_t)t, (uint32_t)i);
             nsp[i] = (u >= c0) ? 1 : 0;
             stl[i] = (uint8_t)st;
@@ -266,6 +439,18 @@ hipError_t launch_ising_mfq(const IsingMfqArgs& a, int R, hipStream_t st) {
         k_ising_mfq<4><<<R, threads, 0, st>>>(a);
     else
         k_ising_mfq<kIsingMaxK><<<R, threads, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_words(uint32_t seed0, int r0, int R, int n_blocks, uint32_t* words, size_t stride, hipStream_t st) {
+    if (R < 1 || n_blocks < 1 || stride < (size_t)n_blocks * kMtN) return hipErrorInvalidValue;
+    k_mt_words<<<(R + 3) / 4, 256, 0, st>>>(seed0, r0, R, n_blocks, words, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_ising_scan(const IsingScanArgs& a, int R, hipStream_t st) {
+    if (a.N < 1 || a.N > kIsingMaxN || a.T < 1 || (a.n_upd < a.N && (!a.mask || !a.perm))) return hipErrorInvalidValue;
+    k_ising_scan<<<R, 64, 0, st>>>(a);
     return hipGetLastError();
 }
 

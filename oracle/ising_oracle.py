@@ -158,3 +158,60 @@ def mfq_loop(n_agents, temperature, steps, lr=0.1, act_rate=1.0, decay_rate=0.99
         return {"q": Q, "order": np.array(orders), "steps": len(orders)}
     finally:
         np.random.set_state(np_state)
+
+
+class MT19937Words:
+    """numpy's legacy MT19937 restated word by word (numpy/random/src/mt19937/mt19937.c: init_genrand seeding of
+    RandomState(seed), the 624-word twist, tempering) with the legacy draws main_MFQ_Ising.py makes, as the device
+    stream (k_mt_words, k_ising_scan) consumes them: choice(2) = one word & 1; random_sample = one double from two
+    words; choice(N, k, replace=False) = the legacy shuffle of arange(N), random_interval by masked rejection.
+    Pure python (test infrastructure: pins that consumption model against numpy itself)."""
+
+    def __init__(self, seed):
+        k = [0] * 624
+        k[0] = seed & 0xFFFFFFFF
+        for i in range(1, 624):
+            k[i] = (1812433253 * (k[i - 1] ^ (k[i - 1] >> 30)) + i) & 0xFFFFFFFF
+        self.key, self.pos, self.count = k, 624, 0
+
+    def _twist(self):
+        k = self.key
+        for i in range(624):
+            y = (k[i] & 0x80000000) | (k[(i + 1) % 624] & 0x7FFFFFFF)
+            k[i] = k[(i + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+        self.pos = 0
+
+    def word(self):
+        if self.pos >= 624:
+            self._twist()
+        y = self.key[self.pos]
+        self.pos += 1
+        self.count += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        y ^= y >> 18
+        return y
+
+    def choice2(self):
+        return self.word() & 1
+
+    def random_sample(self):
+        a, b = self.word() >> 5, self.word() >> 6
+        return (a * 67108864.0 + b) / 9007199254740992.0
+
+    def interval(self, mx):
+        m = mx
+        for s in (1, 2, 4, 8, 16):
+            m |= m >> s
+        while True:
+            v = self.word() & m
+            if v <= mx:
+                return v
+
+    def choice_no_replace(self, n, k):
+        x = list(range(n))
+        for i in range(n - 1, 0, -1):
+            j = self.interval(i)
+            x[i], x[j] = x[j], x[i]
+        return x[:k]

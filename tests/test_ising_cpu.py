@@ -91,3 +91,17 @@ def test_per_agent_loop_restatement_matches_the_vectorised_oracle(n, steps):
     assert a["steps"] == b["steps"]
     assert a["q"].tobytes() == b["q"].tobytes()
     assert a["order"].tobytes() == b["order"].tobytes()
+
+
+@pytest.mark.parametrize("seed,n,k", [(13, 400, 400), (21, 100, 50), (5, 16, 3)])
+def test_numpy_stream_model(seed, n, k):
+    """The consumption model the device stream follows (csrc/ising_kernels.hip k_mt_words / k_ising_scan), restated
+    word by word in oracle/ising_oracle.py MT19937Words, against numpy's own legacy RandomState: the seeding, the
+    choice(2) spins, random_sample's doubles and choice(N, k, replace=False)'s shuffle draws, over two steps."""
+    rs, mt = np.random.RandomState(seed), ising_oracle.MT19937Words(seed)
+    assert list(rs.get_state()[1]) == mt.key
+    assert [int(rs.choice(2)) for _ in range(2 * n)] == [mt.choice2() for _ in range(2 * n)]
+    for _ in range(2):
+        assert rs.random_sample(n).tobytes() == np.array([mt.random_sample() for _ in range(n)]).tobytes()
+        assert list(rs.choice(n, k, replace=False)) == mt.choice_no_replace(n, k)
+    assert rs.randint(0, 2 ** 32, dtype=np.uint64) == mt.word()

@@ -1,8 +1,8 @@
 """Ising lattice + tabular MF-Q on the GPU (through the mfx_ising_* C ABI).
 
-* the fused MF-Q kernel in 'reference' mode reproduces the reference trajectories recorded in
-  tests/golden/ising_*.npz bit for bit: every action, order parameter, n_up, the early-stop
-  step and the float64 Q table;
+* the fused MF-Q kernel in 'reference' mode -- numpy's RandomState stream generated on the device --
+  reproduces the reference trajectories recorded in tests/golden/ising_*.npz bit for bit: every action,
+  order parameter, n_up, the early-stop step and the float64 Q table;
 * the drop-in examples.ising_model env driven by main_MFQ_Ising.py's own loop gives the same;
 * the batched env step matches the numpy oracle on random lattices (R replicas);
 * Philox mode: ordered phase at low temperature, disordered at high temperature."""
@@ -160,3 +160,36 @@ def test_large_lattice_env_step_matches_oracle():
         assert rew[r].tobytes() == rw.tobytes()
         np.testing.assert_array_equal(obs[r], ob)
         assert nup[r] == nu and order[r] == od
+
+
+@pytest.mark.parametrize("n_agents,replicas,steps,act_rate", [(400, 6, 700, 1.0), (100, 3, 300, 0.5),
+                                                              (1600, 2, 50, 1.0), (4, 5, 900, 0.75)])
+def test_device_stream_matches_host_stream(n_agents, replicas, steps, act_rate):
+    """numpy's RandomState stream generated on the device (k_mt_words: MT19937; k_ising_scan: the act_group
+    permutation's rejection walk, the act_group bits when act_rate < 1) against the same stream drawn by numpy on
+    the host and uploaded (mode 'host'): replica r = seed 13 + r; Q, every order parameter, n_up, the stop step and
+    the final spins bit for bit -- including the large-lattice kernel (1600 agents) and a 2x2 lattice whose episodes
+    run to the step cap."""
+    from mfrl_amd.ising import run_mfq
+    dev = run_mfq(n_agents, 0.8, steps, act_rate=act_rate, seed=13, replicas=replicas)
+    host = run_mfq(n_agents, 0.8, steps, act_rate=act_rate, seed=13, replicas=replicas, mode="host")
+    np.testing.assert_array_equal(dev["steps"], host["steps"])
+    for r in range(replicas):
+        T = int(host["steps"][r])
+        assert dev["order"][r, :T].tobytes() == host["order"][r, :T].tobytes(), r
+        np.testing.assert_array_equal(dev["n_up"][r, :T], host["n_up"][r, :T])
+    assert dev["q"].tobytes() == host["q"].tobytes()
+    np.testing.assert_array_equal(dev["spins"], host["spins"])
+
+
+def test_device_stream_many_replicas_match_oracle():
+    """2048 replicas of configs[0] (20x20, tau 0.8) on the device stream in one call (one word-generation pass):
+    sampled replicas against the numpy oracle (oracle/ising_oracle.py mfq, seed 13 + r) bit for bit."""
+    from mfrl_amd.ising import run_mfq
+    R, T = 2048, 600
+    got = run_mfq(400, 0.8, T, seed=13, replicas=R)
+    for r in (0, 1, 777, R - 1):
+        ref = ising_oracle.mfq(400, 0.8, T, seed=13 + r)
+        assert int(got["steps"][r]) == ref["steps"]
+        assert got["order"][r, :ref["steps"]].tobytes() == ref["order"].tobytes()
+        assert got["q"][r].tobytes() == ref["q"].tobytes()
