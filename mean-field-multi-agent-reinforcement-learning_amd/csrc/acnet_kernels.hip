@@ -50,10 +50,58 @@ constexpr int kABlocks = 19;
 // 15 wvd [544][256] MF value dense  16 bvd [256]
 // 17 wvo [256][16] MF value (column 0)                                           18 bvo [16]
 // (blocks 9-10 are empty with mean field, 11-18 without.)
+// The weight images of the GEMM layers (policy_gemm.h wg_gemm_i; made at set_weights by k_acnet_image):
+//  0 wv  1 wd0  2 wd1  3 wp (units 0..255 of d)  4 wp (units 256..511)  5 wval (0..255)  6 wval (256..511)
+//  7 wep  8 wdp  9 wvd  10 wvo
+constexpr int kAImg = 11;
 struct ACNetDev {
     const float* w[kABlocks];
+    const float* img[kAImg];
     int V, Vp, F, Fp, A, Ap, use_mf;
 };
+
+// One weight image: thread per image float -> the source weight (zero past K and in the MT < 4 padding).
+__global__ void __launch_bounds__(256) k_acnet_image(const float* __restrict__ src, int K, int N, float* __restrict__ dst,
+                                                     size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int mt = N / 16, rw = img_row(mt);
+    const int pos = (int)(i % rw), r = (int)((i / rw) % 16);
+    const size_t ch = i / ((size_t)16 * rw);
+    int c, t;
+    if (mt % 4) {
+        c = pos / 4;
+        t = pos % 4;
+    } else {
+        const int G = mt / 4;
+        c = pos / mt;
+        const int rem = pos % mt, slot = rem / 4;
+        t = 4 * ((slot - c * G / 16 + G) % G) + rem % 4;
+    }
+    const size_t k = ch * 16 + r;
+    dst[i] = (t < mt && k < (size_t)K) ? src[k * N + 16 * t + c] : 0.f;
+}
+
+// acc[t] = bias[16 t + 4 h .. + 3] (a layer's accumulators start at its bias: one 16-B load per tile, issued
+// together, instead of one dependent load per unit after the GEMM)
+__device__ __forceinline__ void bias_init(f32x4* acc, const float* bias, int h) {
+    const float4* b = reinterpret_cast<const float4*>(bias) + h;
+    float4 v[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v[t] = b[4 * t];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = {v[t].x, v[t].y, v[t].z, v[t].w};
+}
+
+// x / 0.1f, correctly rounded (the reference's dense / 0.1): q = x * 10, one fma residual and one fma correction --
+// equal to the IEEE quotient for every f32 |x| >= 2^-100 (checked exhaustively, scripts/micro/div_tenth.c); tinier
+// nonzero x take the division.
+__device__ __forceinline__ float div_tenth(float x) {
+    const float q = x * 10.0f, r = __builtin_fmaf(-q, 0.1f, x);
+    float y = __builtin_fmaf(r, 10.0f, q);
+    if (__builtin_expect(x != 0.f && __builtin_fabsf(x) < 0x1p-100f, 0)) y = x / 0.1f;
+    return y;
+}
 
 __device__ __forceinline__ uint32_t ac_mix32(uint32_t h) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
@@ -75,9 +123,15 @@ __device__ __forceinline__ float ac_uniform(uint32_t seed, uint32_t step, int g,
 // where the concat needs it -- 3 % more MFMA work for 64 fewer registers per lane, which is what lets two
 // workgroups share a CU (one wave per SIMD otherwise: 256 VGPRs + ~100 AGPRs).
 constexpr int kHeF = 36;
+#ifndef MFX_ACNET_SKIP
+#define MFX_ACNET_SKIP 0      // A/B builds only (make variant): 1 view layer, 2 dense layers, 4 policy layer, 8 h_emb skipped
+#endif
 constexpr size_t kAcnetLdsSmem = kQHeadSmem + (size_t)kHeF * kAH * 4;
+constexpr size_t kAcnetImgLdsSmem = kImgSmem + (size_t)kHeF * kAH * 4 + 3 * 1024 * 4;   // + the view ring: 80 KB
 
-template <typename PT, bool kMF, bool kHeLds>
+// kImg: the layers run wg_gemm_i over the weight images (direct-to-LDS staging; the default), else wg_gemm_t (A/B:
+// MFX_ACNET_IMG=0).  GEMM<MT, NCH, kZero>(block, image, K, v_at, acc) picks the form.
+template <typename PT, bool kMF, bool kHeLds, bool kImg>
 __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const float* __restrict__ view, size_t view_ld,
                                                   const float* __restrict__ feat, size_t feat_ld,
                                                   const PT* __restrict__ prob, size_t prob_ld, QRowMap rm, int n,
@@ -86,17 +140,73 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
                                                   uint32_t seed, uint32_t step, int group) {
     extern __shared__ __attribute__((aligned(16))) float qsm[];
     if (d_n) n = min(*d_n, n);
-    if ((int)blockIdx.x * kQHeadWaves * 16 >= n) return;           // (uniform: a launch sized for the upper bound)
+    const int tiles = (n + kQHeadWaves * 16 - 1) / (kQHeadWaves * 16);
+    if ((int)blockIdx.x >= tiles) return;                          // (uniform: a launch sized for the upper bound)
     float* bsm = qsm;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
-    const int base = (blockIdx.x * kQHeadWaves + wid) * 16;
+    const bool he_fold = kImg && p.F < kHeF;                       // (kImg: the folded form; A/B keeps the old one)
+    const float* weS = bsm + (kImg ? 2 * kImgBuf : 2 * kQKC * kQBLd);   // kHeLds: We [kHeF][256] after the staging
+    if (kHeLds) {
+        // We in LDS for the workgroup's life; the bias as one more input row when the features leave one free
+        // (k = F: weight be, input 1), so the recomputed tile needs no bias load
+        float* wd = bsm + (kImg ? 2 * kImgBuf : 2 * kQKC * kQBLd);
+        const int F = p.F;
+        for (int i = threadIdx.x; i < kHeF * kAH; i += blockDim.x)
+            wd[i] = i < F * kAH ? p.w[2][i] : (he_fold && i < (F + 1) * kAH) ? p.w[3][i - F * kAH] : 0.f;
+        __syncthreads();
+    }
+    // persistent: tile after tile of 64 agents (the grid: the workgroups the CUs hold at once, or fewer)
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int tid = tid_x(), lane = tid & 63, wid = tid >> 6, h = lane >> 4, c = lane & 15;
+    const int base = (tile * kQHeadWaves + wid) * 16;
     const int ia = min(base + c, n - 1);                            // this lane's agent (clamped: junk, never written)
     const int row = rm.rows ? rm.rows[ia] : ia;
     const int env = rm.rows ? row / rm.rowcap : ia;
-    const float* const* W = p.w;
+    // the weight and image pointers, opaque per tile: else the compiler hoists every chunk's addresses out of the
+    // tile loop and spills them
+    const float* W[kABlocks];
+    const float* I[kAImg];
+#pragma unroll
+    for (int k = 0; k < kABlocks; ++k) { W[k] = p.w[k]; asm volatile("" : "+s"(W[k])); }
+#pragma unroll
+    for (int k = 0; k < kAImg; ++k) { I[k] = p.img[k]; asm volatile("" : "+s"(I[k])); }
+#define MFX_ACNET_GEMM(MT, NCH, ZERO, WB, IB, K, VAT, ACC)                                                              \
+    do {                                                                                                              \
+        if constexpr (kImg) wg_gemm_i<MT, NCH, ZERO>(IB, K, VAT, bsm, ACC);                                          \
+        else wg_gemm_t<MT, NCH, ZERO>(WB, K, VAT, bsm, ACC);                                                         \
+    } while (0)
     // ---- h_view^T [256 x 16]: view floats k = 16 ch + 4 h + s of this lane's agent, two chunks ahead in flight
     f32x4 hv[16];
-    {
+    if constexpr (kImg) {
+        // the view rows through LDS: a ring of 3 chunks (64 agents x 16 floats each, after We), filled two chunks
+        // ahead by direct-to-LDS loads -- instruction q of wave w: agent 4 (4 w + q) + lane / 16, float lane % 16
+        // (columns past V read float V - 1: its weights are zero)
+        float* vring = bsm + 2 * kImgBuf + kHeF * kAH;
+        const float* vsrc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = min(tile * kQHeadWaves * 16 + 4 * (4 * wid + q) + (lane >> 4), n - 1);
+            vsrc[q] = view + (size_t)(rm.rows ? rm.rows[a] : a) * view_ld;
+        }
+        const int V = p.V;
+        auto view_issue = [&](int ch) {
+            float* dst = vring + (ch % 3) * 1024 + wid * 256;
+            const int k = min(16 * ch + c, V - 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_global_load_lds((const void*)(vsrc[q] + k),
+                                                 (__attribute__((address_space(3))) void*)(dst + q * 64), 4, 0, 0);
+        };
+        view_issue(0);
+        view_issue(1);
+        float4 xv;
+        auto vat = [&](int ch, int s) {
+            if (s == 0) xv = reinterpret_cast<const float4*>(vring + (ch % 3) * 1024)[(16 * wid + c) * 4 + h];
+            return s == 0 ? xv.x : s == 1 ? xv.y : s == 2 ? xv.z : xv.w;
+        };
+        bias_init(hv, W[1], h);
+        if (!(MFX_ACNET_SKIP & 1))
+            wg_gemm_i<16, 0, false, 4>(I[0], p.Vp, vat, bsm, hv, [&](int ch) { view_issue(ch + 2); });
+    } else {
         const float* vr = view + (size_t)row * view_ld + 4 * h;
         const int V = p.V;
         float b0[4], b1[4], b2[4];
@@ -110,7 +220,7 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
         fetch(0, b0);
         fetch(1, b1);
         int have = -1;
-        wg_gemm_t<16>(W[0], p.Vp, [&](int ch, int s) {
+        auto vat = [&](int ch, int s) {
             if (s == 0 && have != ch) {                             // rotate: chunk ch in b0, ch + 1 in b1
                 if (have >= 0) {
 #pragma unroll
@@ -120,49 +230,55 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
                 fetch(ch + 2, b2);
             }
             return b0[s];
-        }, bsm, hv);
+        };
+        bias_init(hv, W[1], h);
+        wg_gemm_t<16, 0, false>(W[0], p.Vp, vat, bsm, hv);
     }
-    // the concat's h_view half, activated in place once (relu(acc + bias)): read as is by every later layer
+    // the concat's h_view half, activated in place once (relu; the bias was the accumulators' start): read as is by
+    // every later layer
 #pragma unroll
     for (int t = 0; t < 16; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hv[t][r] = relu_unit(hv, W[1], t, r);
+        for (int r = 0; r < 4; ++r) hv[t][r] = fmaxf(hv[t][r], 0.f);
     // ---- h_emb^T [256 x 16]: held (kHeLds false), or recomputed per tile from the LDS-resident weights
     f32x4 he[kHeLds ? 1 : 16];
     float fr4[kHeLds ? kHeF / 4 : 1];
-    const float* weS = bsm + 2 * kQKC * kQBLd;                      // kHeLds: We [kHeF][256] after the staging
     {
         const float* fr = feat + (size_t)row * feat_ld;
         const int F = p.F;
         if (kHeLds) {
-            float* wd = bsm + 2 * kQKC * kQBLd;
-            for (int i = threadIdx.x; i < kHeF * kAH; i += blockDim.x) wd[i] = i < p.Fp * kAH ? W[2][i] : 0.f;
 #pragma unroll
             for (int ks = 0; ks < kHeF / 4; ++ks) {                 // k = 4 ks + h: this lane's B operands
                 const int k = 4 * ks + h;
-                fr4[ks] = k < F ? fr[k] : 0.f;
+                fr4[ks] = k < F ? fr[k] : (he_fold && k == F) ? 1.f : 0.f;
             }
-            __syncthreads();
         } else {
             wg_gemm_t<16>(W[2], p.Fp, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < F ? fr[k] : 0.f; },
-                          bsm, he);
+                          bsm, he);                                 // (small K: registers staging either way)
         }
     }
-    // h_emb tile t (units 16 t + 4 h + r in register r, agent c): A = We^T rows 16 t + c from LDS, B = the features
-    auto he_tile = [&](int t) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // h_emb tile t (units 16 t + 4 h + r in register r, agent c): A = We^T rows 16 t + c from LDS, B = the features.
+    // Software-pipelined: tile t's 9 dependent MFMAs run spread over the four k-steps of the chunk before the one
+    // that reads it (3 + 2 + 2 + 2, each behind the chunk's 16 independent MFMAs), not as a chain at its head.
+    static_assert(kHeF == 36, "the k-step split of the h_emb tile");
+    f32x4 he_cur = {0.f, 0.f, 0.f, 0.f}, he_nxt = {0.f, 0.f, 0.f, 0.f};
+    auto he_part = [&](int t, int s) {
+        const int lo = s == 0 ? 0 : 1 + 2 * s, hi = 3 + 2 * s;
 #pragma unroll
-        for (int ks = 0; ks < kHeF / 4; ++ks) acc = mfma4(weS[(4 * ks + h) * kAH + 16 * t + c], fr4[ks], acc);
-        return acc;
+        for (int ks = lo; ks < hi; ++ks) he_nxt = mfma4(weS[(4 * ks + h) * kAH + 16 * t + c], fr4[ks], he_nxt);
     };
-    f32x4 he_cur = {0.f, 0.f, 0.f, 0.f};
-    // concat unit k = 16 ch + 4 h + s: ch < 16 h_view tile ch, else h_emb tile ch - 16
+    // concat unit k = 16 ch + 4 h + s: ch < 16 h_view tile ch, else h_emb tile ch - 16 (calls in (ch, s) order)
     auto concat_at = [&](int ch, int s) {
-        if (ch < 16) return hv[ch][s];
+        if (MFX_ACNET_SKIP & 8) return hv[ch & 15][s];
         if (kHeLds) {
-            if (s == 0) he_cur = he_tile(ch - 16);
-            return relu_unit(&he_cur, W[3] + 16 * (ch - 16), 0, s);
+            if (ch >= 16 && s == 0) he_cur = he_nxt;
+            if (ch >= 15 && ch < 31) {
+                if (s == 0) he_nxt = {0.f, 0.f, 0.f, 0.f};
+                he_part(ch - 15, s);
+            }
         }
+        if (ch < 16) return hv[ch][s];
+        if (kHeLds) return he_fold ? fmaxf(he_cur[s], 0.f) : relu_unit(&he_cur, W[3] + 16 * (ch - 16), 0, s);
         return relu_unit(he, W[3], ch - 16, s);
     };
     // ---- dense [512] in two halves, each folded into the policy logits (and the AC value) at once
@@ -170,35 +286,41 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
     f32x4 vv[1] = {{0.f, 0.f, 0.f, 0.f}};
     {
         f32x4 dh[16];
-        auto act_half = [&](int half) {                             // relu(acc + bias) in place
+        auto act_half = [&](int half) {                             // relu in place (the bias: the GEMM's start)
 #pragma unroll
             for (int t = 0; t < 16; ++t)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) dh[t][r] = relu_unit(dh, W[6] + half * kAH, t, r);
+                for (int r = 0; r < 4; ++r) dh[t][r] = fmaxf(dh[t][r], 0.f);
         };
-        wg_gemm_t<16, 32>(W[4], 2 * kAH, concat_at, bsm, dh);
+        auto dsc = [&](int ch, int s) { return div_tenth(dh[ch][s]); };
+        auto dval = [&](int ch, int s) { return dh[ch][s]; };
+        bias_init(dh, W[6], h);
+        if (!(MFX_ACNET_SKIP & 2)) MFX_ACNET_GEMM(16, 32, false, W[4], I[1], 2 * kAH, concat_at, dh);
         act_half(0);
-        wg_gemm_t<2, 16, true>(W[7], kAH, [&](int ch, int s) { return dh[ch][s] / 0.1f; }, bsm, pl);
-        if (!kMF && value_out) wg_gemm_t<1, 16, true>(W[9], kAH, [&](int ch, int s) { return dh[ch][s]; }, bsm, vv);
-        wg_gemm_t<16, 32>(W[5], 2 * kAH, concat_at, bsm, dh);
+        if (!(MFX_ACNET_SKIP & 4)) MFX_ACNET_GEMM(2, 16, true, W[7], I[3], kAH, dsc, pl);
+        else pl[0] = pl[1] = dh[0];
+        if (!kMF && value_out) MFX_ACNET_GEMM(1, 16, true, W[9], I[5], kAH, dval, vv);
+        bias_init(dh, W[6] + kAH, h);
+        if (!(MFX_ACNET_SKIP & 2)) MFX_ACNET_GEMM(16, 32, false, W[5], I[2], 2 * kAH, concat_at, dh);
         act_half(1);
-        wg_gemm_t<2, 16, false>(W[7] + kAH * kAMaxA, kAH, [&](int ch, int s) { return dh[ch][s] / 0.1f; }, bsm, pl);
-        if (!kMF && value_out)
-            wg_gemm_t<1, 16, false>(W[9] + kAH * 16, kAH, [&](int ch, int s) { return dh[ch][s]; }, bsm, vv);
+        if (!(MFX_ACNET_SKIP & 4)) MFX_ACNET_GEMM(2, 16, false, W[7] + kAH * kAMaxA, I[4], kAH, dsc, pl);
+        else pl[0] += dh[1];
+        if (!kMF && value_out) MFX_ACNET_GEMM(1, 16, false, W[9] + kAH * 16, I[6], kAH, dval, vv);
     }
     // ---- MF value: emb_prob 64, dense_prob 32, dense 256 over concat(h_view, h_emb, p), value 1
     if (kMF && value_out) {
         const PT* pr = prob + (size_t)env * prob_ld;
         const int A = p.A;
         f32x4 e1[4], e2[2];
-        wg_gemm_t<4>(W[11], p.Ap, [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < A ? (float)pr[k] : 0.f; },
-                     bsm, e1);
-        wg_gemm_t<2, 4>(W[13], 64, [&](int ch, int s) { return relu_unit(e1, W[12], ch, s); }, bsm, e2);
+        auto pat = [&](int ch, int s) { const int k = 16 * ch + 4 * h + s; return k < A ? (float)pr[k] : 0.f; };
+        MFX_ACNET_GEMM(4, 0, true, W[11], I[7], p.Ap, pat, e1);
+        auto e1at = [&](int ch, int s) { return relu_unit(e1, W[12], ch, s); };
+        MFX_ACNET_GEMM(2, 4, true, W[13], I[8], 64, e1at, e2);
         f32x4 vd[16];
-        wg_gemm_t<16, 34>(W[15], 2 * kAH + 32, [&](int ch, int s) {
-            return ch < 32 ? concat_at(ch, s) : relu_unit(e2, W[14], ch - 32, s);
-        }, bsm, vd);
-        wg_gemm_t<1, 16>(W[17], kAH, [&](int ch, int s) { return relu_unit(vd, W[16], ch, s); }, bsm, vv);
+        auto vdat = [&](int ch, int s) { return ch < 32 ? concat_at(ch, s) : relu_unit(e2, W[14], ch - 32, s); };
+        MFX_ACNET_GEMM(16, 34, true, W[15], I[9], 2 * kAH + 32, vdat, vd);
+        auto voat = [&](int ch, int s) { return relu_unit(vd, W[16], ch, s); };
+        MFX_ACNET_GEMM(1, 16, true, W[17], I[10], kAH, voat, vv);
     }
     const int i = base + c;
     if (value_out && h == 0 && i < n) value_out[i] = vv[0][0] + W[kMF ? 18 : 10][0];   // unit 0: lanes h == 0, r 0
@@ -247,6 +369,9 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
             act_out[slot] = pick;
         }
     }
+    __syncthreads();                                                 // (lg and the staging buffers: the next tile's)
+    }
+#undef MFX_ACNET_GEMM
 }
 
 }  // namespace mfx
@@ -259,7 +384,22 @@ struct ACNetHandle {
     ACNetDev dev{};
     float* blob = nullptr;
     size_t blob_n = 0;
+    float* img = nullptr;                 // the weight images (k_acnet_image), made by set_weights
+    size_t img_n = 0;
+    bool imaged = false;
 };
+
+// The imaged blocks: (blob block, row offset, K, N) of images 0..10 (ACNetDev::img).
+struct ImgDesc { int block, row0, K, N; };
+void acnet_images(const ACNetDev& d, ImgDesc* o) {
+    const int mf = d.use_mf;
+    const ImgDesc t[kAImg] = {{0, 0, d.Vp, kAH}, {4, 0, 2 * kAH, kAH}, {5, 0, 2 * kAH, kAH},
+                              {7, 0, kAH, kAMaxA}, {7, kAH, kAH, kAMaxA},
+                              {9, 0, mf ? 0 : kAH, 16}, {9, kAH, mf ? 0 : kAH, 16},
+                              {11, 0, mf ? d.Ap : 0, 64}, {13, 0, mf ? 64 : 0, 32},
+                              {15, 0, mf ? 2 * kAH + 32 : 0, kAH}, {17, 0, mf ? kAH : 0, 16}};
+    for (int k = 0; k < kAImg; ++k) o[k] = t[k];
+}
 
 void acnet_sizes(int V, int F, int A, int use_mf, size_t* sz) {
     const size_t Vp = (V + 3) & ~3, Fp = (F + 3) & ~3, Ap = (A + 3) & ~3;
@@ -299,6 +439,17 @@ MFX_API int mfx_acnet_create(int view_floats, int feature, int n_action, int use
     q->dev.F = feature; q->dev.Fp = (feature + 3) & ~3;
     q->dev.A = n_action; q->dev.Ap = (n_action + 3) & ~3;
     q->dev.use_mf = use_mf ? 1 : 0;
+    ImgDesc im[kAImg];
+    acnet_images(q->dev, im);
+    size_t io[kAImg], tot = 0;
+    for (int k = 0; k < kAImg; ++k) { io[k] = tot; tot += im[k].K ? img_floats(im[k].K, im[k].N / 16) : 0; }
+    if (hipMalloc(&q->img, tot * sizeof(float)) != hipSuccess) {
+        (void)hipFree(q->blob);
+        delete q;
+        return fail("acnet: hipMalloc of %zu image floats", tot);
+    }
+    q->img_n = tot;
+    for (int k = 0; k < kAImg; ++k) q->dev.img[k] = q->img + io[k];
     *handle = q;
     return 0;
 }
@@ -307,6 +458,7 @@ MFX_API int mfx_acnet_destroy(void* handle) {
     auto* q = static_cast<ACNetHandle*>(handle);
     if (!q) return 0;
     if (q->blob) (void)hipFree(q->blob);
+    if (q->img) (void)hipFree(q->img);
     delete q;
     return 0;
 }
@@ -315,6 +467,16 @@ MFX_API int mfx_acnet_set_weights(void* handle, const float* d_blob, size_t n_fl
     auto* q = static_cast<ACNetHandle*>(handle);
     if (n_floats != q->blob_n) return fail("acnet_set_weights: %zu floats, the layout has %zu", n_floats, q->blob_n);
     MFX_HIP(hipMemcpyAsync(q->blob, d_blob, n_floats * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    ImgDesc im[kAImg];
+    acnet_images(q->dev, im);
+    for (int k = 0; k < kAImg; ++k) {
+        if (!im[k].K) continue;
+        const size_t n = img_floats(im[k].K, im[k].N / 16);
+        k_acnet_image<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+            q->dev.w[im[k].block] + (size_t)im[k].row0 * im[k].N, im[k].K, im[k].N, const_cast<float*>(q->dev.img[k]), n);
+        MFX_HIP(hipGetLastError());
+    }
+    q->imaged = true;
     return 0;
 }
 
@@ -323,16 +485,32 @@ static int acnet_run(ACNetHandle* q, const float* view, size_t view_ld, const fl
                      float* policy, float* value, int32_t* act, uint32_t seed, uint32_t step, int group, hipStream_t st) {
     if (n <= 0) return 0;
     if (q->dev.use_mf && value && !prob) return fail("acnet: the mean-field value head needs prob");
-    const int grid = (n + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
+    // persistent workgroups: as many as the CUs hold at once (two per CU with h_emb in LDS), at most one per tile
+    int grid = (n + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
     const char* hl = getenv("MFX_ACNET_HE_LDS");                    // A/B only: 0 = h_emb held in registers
     const bool lds = q->dev.Fp <= kHeF && !(hl && atoi(hl) == 0);
+    const char* il = getenv("MFX_ACNET_IMG");                       // A/B only: 0 = wg_gemm_t's register staging
+    const bool img = q->imaged && !(il && atoi(il) == 0);
+    {
+        const char* pl = getenv("MFX_ACNET_PERSIST");               // A/B only: 0 = one workgroup per tile
+        if (!(pl && atoi(pl) == 0)) grid = std::min(grid, (lds ? 2 : 1) * device_cus());
+    }
+#define MFX_ACNET_LAUNCH1(PT, MF, LDS, IMG, PB)                                                                         \
+    k_acnet<PT, MF, LDS, IMG><<<grid, 256, IMG && LDS ? kAcnetImgLdsSmem : (LDS ? kAcnetLdsSmem : kQHeadSmem),         \
+                                st>>>(q->dev, view, view_ld, feat, feat_ld, PB, prob_ld, rm, n, d_n, policy, value, act,  \
+                                      seed, step, group)
 #define MFX_ACNET_LAUNCH(PT, MF, LDS, PB)                                                                              \
-    k_acnet<PT, MF, LDS><<<grid, 256, LDS ? kAcnetLdsSmem : kQHeadSmem, st>>>(q->dev, view, view_ld, feat, feat_ld, PB, \
-                                                                            prob_ld, rm, n, d_n, policy, value, act,   \
-                                                                            seed, step, group)
+    do {                                                                                                              \
+        if (img) MFX_ACNET_LAUNCH1(PT, MF, LDS, true, PB);                                                            \
+        else MFX_ACNET_LAUNCH1(PT, MF, LDS, false, PB);                                                               \
+    } while (0)
     const double* pd = static_cast<const double*>(prob);
     const float* pf = static_cast<const float*>(prob);
-    if (q->dev.use_mf && prob_f64) {
+    // (kMF selects only the value head: without value_out both forms compute the same policy, and the plain one
+    // holds fewer registers)
+    if (!value) {
+        if (lds) MFX_ACNET_LAUNCH(float, false, true, pf); else MFX_ACNET_LAUNCH(float, false, false, pf);
+    } else if (q->dev.use_mf && prob_f64) {
         if (lds) MFX_ACNET_LAUNCH(double, true, true, pd); else MFX_ACNET_LAUNCH(double, true, false, pd);
     } else if (q->dev.use_mf) {
         if (lds) MFX_ACNET_LAUNCH(float, true, true, pf); else MFX_ACNET_LAUNCH(float, true, false, pf);
@@ -340,6 +518,7 @@ static int acnet_run(ACNetHandle* q, const float* view, size_t view_ld, const fl
         if (lds) MFX_ACNET_LAUNCH(float, false, true, pf); else MFX_ACNET_LAUNCH(float, false, false, pf);
     }
 #undef MFX_ACNET_LAUNCH
+#undef MFX_ACNET_LAUNCH1
     MFX_HIP(hipGetLastError());
     return 0;
 }

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -27,6 +29,7 @@ struct IsingEngine {
     DevBuf<uint32_t> words, off[2];          // the device stream (mfx_ising_mfq_run_stream)
     DevBuf<uint16_t> perm;
     DevBuf<int32_t> err;
+    DevBuf<unsigned long long> scan_stats;   // MFX_ISING_SCAN_STATS diagnostics
     ~IsingEngine() { if (stream) (void)hipStreamDestroy(stream); }
 };
 
@@ -155,8 +158,8 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
     const int n_upd = (int)(act_rate * N);                  // int(act_rate * n_agents), main_MFQ_Ising.py:126
     // words per replica: make_world's N, then per episode N spins and per step 2 N uniforms + the permutation's
     // draws (N - 1 accepted words plus rejections: ~0.5 N expected, bounded here by 2 N -- a walk past the end sets
-    // the error word) + one chunk of read-ahead
-    const size_t per = (size_t)N + (size_t)episodes * ((size_t)N + (size_t)T * 4 * N) + 64;
+    // the error word) + one chunk of read-ahead (k_ising_scan reads 64 words at a time; its prefetch clamps at the stride)
+    const size_t per = (size_t)N + (size_t)episodes * ((size_t)N + (size_t)T * 4 * N) + 320;
     const int blocks = (int)((per + 623) / 624);
     const size_t W = (size_t)blocks * 624;
     // replicas per pass: the word streams within ~16 GB
@@ -176,6 +179,12 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
         return mfx::fail("%s", ex.what());
     }
     MFX_HIP(hipMemsetAsync(e->err.p, 0, sizeof(int32_t), e->stream));
+    const char* ss = getenv("MFX_ISING_SCAN_STATS");                // diagnostics only
+    const bool want_stats = ss && atoi(ss) != 0;
+    if (want_stats) {
+        try { e->scan_stats.ensure(4); } catch (const std::exception& ex) { return mfx::fail("%s", ex.what()); }
+        MFX_HIP(hipMemsetAsync(e->scan_stats.p, 0, 4 * sizeof(unsigned long long), e->stream));
+    }
     for (int r0 = 0; r0 < R; r0 += Rb) {
         const int nr = std::min(Rb, R - r0);
         MFX_HIP(mfx::launch_mt_words(seed0, r0, nr, blocks, e->words.p, W, e->stream));
@@ -189,6 +198,11 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
             sa.mask = n_upd < N ? e->mask.p : nullptr;
             sa.perm = n_upd < N ? e->perm.p : nullptr;
             sa.err = e->err.p;
+            sa.stats = want_stats ? e->scan_stats.p : nullptr;
+            {
+                const char* rb = getenv("MFX_ISING_SCAN_RING");              // A/B only: 16 / 32 blocks
+                sa.ring = rb ? atoi(rb) : 32;
+            }
             MFX_HIP(mfx::launch_ising_scan(sa, nr, e->stream));
             mfx::IsingMfqArgs a{};
             a.N = N; a.K = K; a.T = T; a.nbr = e->nbr.p; a.spins0 = e->spins.p + (size_t)r0 * N;
@@ -214,6 +228,13 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
     int32_t err = 0;
     MFX_HIP(hipMemcpyAsync(&err, e->err.p, sizeof(err), hipMemcpyDeviceToHost, e->stream));
     MFX_HIP(hipStreamSynchronize(e->stream));
+    if (want_stats) {
+        unsigned long long st[4] = {};
+        MFX_HIP(hipMemcpy(st, e->scan_stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        fprintf(stderr, "ising scan: %llu chunks, %.3f passes per chunk, %.2f words per chunk, %llu wave-reads past "
+                        "the window\n", st[0], st[0] ? (double)st[1] / st[0] : 0.0, st[0] ? (double)st[3] / st[0] : 0.0,
+                st[2]);
+    }
     if (err) return mfx::fail("ising mfq stream: a replica's draws ran past its %zu generated words", W);
     return 0;
 }

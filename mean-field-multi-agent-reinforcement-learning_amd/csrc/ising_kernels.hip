@@ -107,20 +107,17 @@ __device__ __forceinline__ double mt_uniform(const uint32_t* p) {
     const uint32_t a = p[0] >> 5, b = p[1] >> 6;
     return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
 }
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// One wave per replica, four replicas per workgroup: the state in LDS.  A twist in three passes whose reads all
-// precede their writes: i < 227 reads key[i + 1], key[i + 397] as they were; 227 <= i < 454 reads key[i - 227] of the
-// first pass; the rest reads key[i - 227] of the second and, for i = 623, key[0] of the first.  Each block of 624
-// words is tempered and stored in order: words[r][624 b ...] is the replica's stream from its first draw.
-__global__ void __launch_bounds__(256) k_mt_words(uint32_t seed0, int r0, int R, int n_blocks, uint32_t* __restrict__ words,
+// One 256-lane workgroup per replica, the state in LDS: a twist in three passes of at most 227 lanes whose reads all
+// precede their writes (a barrier between): i < 227 reads key[i + 1], key[i + 397] as they were; 227 <= i < 454
+// reads key[i - 227] of the first pass; the rest reads key[i - 227] of the second and, for i = 623, key[0] of the
+// first.  Each block of 624 words is tempered and stored in order: words[r][624 b ...] is the replica's stream from
+// its first draw.  (One wave per replica ran each block ~2x longer: the block chain is the replica's latency.)
+__global__ void __launch_bounds__(256) k_mt_words(uint32_t seed0, int r0, int n_blocks, uint32_t* __restrict__ words,
                                                   size_t stride) {
-    __shared__ uint32_t st[4][kMtN];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + wv;
-    if (r >= R) return;                       // (a whole wave: no workgroup barrier below)
-    uint32_t* mt = st[wv];
-    if (lane == 0) {
+    __shared__ uint32_t mt[kMtN];
+    const int r = blockIdx.x, t = threadIdx.x;
+    if (t == 0) {
         uint32_t x = seed0 + (uint32_t)(r0 + r);
         mt[0] = x;
         for (int i = 1; i < kMtN; ++i) {
@@ -128,60 +125,46 @@ __global__ void __launch_bounds__(256) k_mt_words(uint32_t seed0, int r0, int R,
             mt[i] = x;
         }
     }
-    wave_lds_fence();
+    __syncthreads();
     uint32_t* out = words + (size_t)r * stride;
     for (int b = 0; b < n_blocks; ++b) {
-        uint32_t v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = lane + 64 * k;
-            if (i < 227) v[k] = mt_next(mt[i], mt[i + 1], mt[i + 397]);
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = lane + 64 * k;
-            if (i < 227) mt[i] = v[k];
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = 227 + lane + 64 * k;
-            if (i < 454) v[k] = mt_next(mt[i], mt[i + 1], mt[i - 227]);
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = 227 + lane + 64 * k;
-            if (i < 454) mt[i] = v[k];
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int i = 454 + lane + 64 * k;
-            if (i < kMtN) v[k] = mt_next(mt[i], mt[i == kMtN - 1 ? 0 : i + 1], mt[i - 227]);
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int i = 454 + lane + 64 * k;
-            if (i < kMtN) mt[i] = v[k];
-        }
-        wave_lds_fence();
-        for (int i = lane; i < kMtN; i += 64) out[(size_t)b * kMtN + i] = mt_temper(mt[i]);
+        uint32_t v = 0;
+        if (t < 227) v = mt_next(mt[t], mt[t + 1], mt[t + 397]);
+        __syncthreads();
+        if (t < 227) mt[t] = v;
+        __syncthreads();
+        const int i2 = 227 + t;
+        if (i2 < 454) v = mt_next(mt[i2], mt[i2 + 1], mt[i2 - 227]);
+        __syncthreads();
+        if (i2 < 454) mt[i2] = v;
+        __syncthreads();
+        const int i3 = 454 + t;
+        if (i3 < kMtN) v = mt_next(mt[i3], mt[i3 == kMtN - 1 ? 0 : i3 + 1], mt[i3 - 227]);
+        __syncthreads();
+        if (i3 < kMtN) mt[i3] = v;
+        __syncthreads();
+        for (int i = t; i < kMtN; i += 256) out[(size_t)b * kMtN + i] = mt_temper(mt[i]);
     }
 }
 
 // One wave per replica: one episode of main_MFQ_Ising.py's draws over the replica's word stream -- env.reset's N
 // spins (choice(2)), then per step the offset of its N uniforms (2 N words) and the act_group permutation's words.
-// The permutation's draws are walked 64 words at a time: lane j holds word j of the chunk; a_j, the draws accepted
-// before it, is the fixed point of a_j = #{l < j : word l accepted when it serves draw m - a_l} (a ballot and a
-// lane count per pass, from the guess a_j = j).  The recursion is triangular -- a_j depends on lanes below j -- so
-// the fixed point is unique and pass k fixes lane k at the latest; a word's decision changes only when its
-// threshold falls between two guesses, so in practice a chunk settles in a few passes.  The chunk ends at the lane
-// that accepts draw 1.  n_upd < N (act_rate < 1): lane 0 also applies the swaps to arange(N) in perm and the first
+// The permutation's draws are walked 64 words at a time (word j in lane j).  Word j serves draw m0 - a_j, a_j the
+// draws accepted before it, and is taken iff (w_j & mask(m0 - a_j)) <= m0 - a_j.  a_j is solved as a fixed point over
+// the lanes (a ballot and a lane count per pass, from a guess at the draw's acceptance rate): the recursion is
+// triangular, so the fixed point is unique and pass k fixes lane k at the latest, and a decision changes only when its
+// threshold falls between two guesses -- ~3.5 passes per chunk.  (A scalar walk over the 64 thresholds -- v_readlane,
+// compare, add-carry -- measured 2.7x slower: every readlane waits on the VALU; a chunk that ends where the mask
+// halves, 1.3x slower.)  The chunk ends at 64 words or at draw 1.  n_upd < N (act_rate < 1): lane 0 also applies the
+// swaps to arange(N) in perm and the first
 // n_upd entries set the step's act_group bits.
+// The permutation's words come from an LDS ring of RB blocks of 64 words (the uniforms are never fetched: k_ising_mfq
+// reads them): each step's blocks are fetched by direct-to-LDS loads (global_load_lds) while the step before walks.
+// The ring is the kernel's occupancy -- one wave per replica, latency-bound, so the waves per CU are its rate: RB = 32
+// (8 KB, 20 waves per CU) holds a step and the next at N = 400; words outside the ring are read from memory.
+template <int RB>
 __global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[RB * 64];
     const int r = blockIdx.x, lane = threadIdx.x;
     const uint32_t* W = a.words + (size_t)r * a.wstride;
     const size_t cap = a.wstride;
@@ -190,26 +173,71 @@ __global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
     uint16_t* x = perm ? a.perm + (size_t)r * N : nullptr;
     uint32_t* off = a.off + (size_t)r * (T + 1);
     bool over = false;
-    auto word = [&](size_t p) -> uint32_t {
+    auto fetch = [&](size_t b0, size_t b1) {                 // issue blocks [b0, b1) into the ring (async)
+#pragma nounroll
+        for (size_t b = b0; b < b1; ++b) {
+            const size_t p = b * 64 + lane;
+            // (a 1- or 2-byte LDS-DMA would not shrink the ring: gfx950 writes each lane's bytes zero-extended to a
+            // dword at base + 4 lane -- scripts/micro/glds_width.hip)
+            __builtin_amdgcn_global_load_lds((const void*)(W + (p < cap ? p : 0)),
+                                             (__attribute__((address_space(3))) void*)(ring + (b % RB) * 64), 4, 0, 0);
+        }
+    };
+    unsigned long long n_chunk = 0, n_pass = 0, n_far = 0, n_word = 0;
+    auto word = [&](size_t p, size_t blo, size_t bhi) -> uint32_t {
         if (p >= cap) { over = true; return 0u; }
+        const size_t b = p >> 6;
+        if (b >= blo && b < bhi) return ring[(b % RB) * 64 + (p & 63)];
+        ++n_far;
         return W[p];
     };
     // the episode's first draw: after make_world's N choice(2) draws, or where the previous episode stopped
     size_t pos = a.prev_off ? a.prev_off[(size_t)r * (T + 1) + a.prev_steps[r]] : (size_t)N;
-    for (int i = lane; i < N; i += 64) a.spins0[(size_t)r * N + i] = (uint8_t)(word(pos + i) & 1u);
+    for (int i = lane; i < N; i += 64) {
+        const size_t p = pos + i;
+        if (p >= cap) over = true;
+        a.spins0[(size_t)r * N + i] = (uint8_t)((p < cap ? W[p] : 0u) & 1u);
+    }
     pos += N;
+    // [vlo, vhi): the blocks complete in the ring; [plo, phi): the blocks in flight.  A fetch may land in the slots of
+    // blocks below phi - RB at any time, so those leave the valid range as it is issued.
+    size_t vlo = 0, vhi = 0, plo = (pos + 2 * (size_t)N) >> 6, phi = (pos + 4 * (size_t)N + 127) >> 6;
+    if (phi > plo + RB) phi = plo + RB;
+    fetch(plo, phi);                                         // step 0's permutation starts at pos + 2 N
     for (int t = 0; t < T; ++t) {
         if (lane == 0) off[t] = (uint32_t)pos;
         pos += 2 * (size_t)N;                                 // the Boltzmann uniforms (k_ising_mfq reads them)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the blocks in flight have landed
+        if (phi > plo) {
+            if (plo <= vhi && plo >= vlo) { if (phi > vhi) vhi = phi; }
+            else { vlo = plo; vhi = phi; }
+            if (vhi > RB && vlo < vhi - RB) vlo = vhi - RB;
+        }
+        // step t + 1's permutation starts 3 N - 1 .. 4 N words past this one's and takes at most 2 N (+ one chunk of
+        // read-ahead; a longer walk reads its tail from memory): in flight while this step walks, never more than
+        // RB blocks above this step's first
+        plo = (pos + 3 * (size_t)N - 1) >> 6;
+        if (plo < vhi) plo = vhi;
+        phi = (pos + 6 * (size_t)N + 127) >> 6;
+        if (phi > (pos >> 6) + RB) phi = (pos >> 6) + RB;
+        if (t + 1 < T && phi > plo) {
+            fetch(plo, phi);
+            if (phi > RB && vlo < phi - RB) vlo = phi - RB;
+        } else {
+            phi = plo;
+        }
+        const size_t blo = vlo, bhi = vhi;
         if (perm && lane == 0)
             for (int i = 0; i < N; ++i) x[i] = (uint16_t)i;
         int m = N - 1;                                       // random_interval(m), m = N-1 .. 1
         while (m >= 1) {
-            const uint32_t w = word(pos + lane);
-            int acc = 0, aj = lane;
+            const uint32_t w = word(pos + lane, blo, bhi);
+            // the guess: lane j's share of accepted words at draw m's acceptance rate (m + 1) / (mask(m) + 1)
+            const float q = (float)(m + 1) / ((float)(0xFFFFFFFFu >> __builtin_clz((uint32_t)m)) + 1.0f);
+            int aj = (int)((float)lane * q), acc = 0;
             unsigned long long bal = 0;
             for (int it = 0; it <= 64; ++it) {
-                const int mm = m - aj;
+                const int mm = m - aj;                       // the draw word j serves, and its mask
                 const uint32_t M = mm >= 1 ? (0xFFFFFFFFu >> __builtin_clz((uint32_t)mm)) : 0u;
                 acc = (mm < 1 || (w & M) <= (uint32_t)mm) ? 1 : 0;
                 bal = __ballot(acc);
@@ -217,16 +245,18 @@ __global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
                 const bool settled = __ballot(an != aj) == 0ull;
                 aj = an;
+                ++n_pass;
                 if (settled) break;
             }
-            const unsigned long long fin = __ballot(aj + acc >= m);   // the lane accepting draw 1, and after
+            ++n_chunk;
+            const unsigned long long fin = __ballot(aj + acc >= m);   // the word accepting draw 1, and after
             const int used = fin ? __builtin_ctzll(fin) + 1 : 64;
             if (perm) {                                      // the swaps in draw order (lane 0, one by one)
                 const int mm = m - aj;
                 const uint32_t jv = mm >= 1 ? (w & (0xFFFFFFFFu >> __builtin_clz((uint32_t)mm))) : 0u;
                 for (int l = 0; l < used; ++l) {
-                    const int al = __shfl(acc, l), ml = __shfl(mm, l);
-                    const int jl = (int)__shfl((int)jv, l);
+                    const int al = __builtin_amdgcn_readlane(acc, l), ml = __builtin_amdgcn_readlane(mm, l);
+                    const int jl = __builtin_amdgcn_readlane((int)jv, l);
                     if (lane == 0 && al && ml >= 1) {
                         const uint16_t xi = x[ml], xj = x[jl];
                         x[ml] = xj;
@@ -235,6 +265,7 @@ __global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
                 }
             }
             pos += used;
+            n_word += used;
             m = fin ? 0 : m - __popcll(bal);
         }
         if (perm) {
@@ -248,8 +279,15 @@ __global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
             }
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) off[T] = (uint32_t)pos;
     if (__ballot(over) && lane == 0) atomicExch(a.err, 1);
+    if (a.stats && lane == 0) {
+        atomicAdd(a.stats, n_chunk);
+        atomicAdd(a.stats + 1, n_pass);
+        atomicAdd(a.stats + 2, n_far);
+        atomicAdd(a.stats + 3, n_word);
+    }
 }
 
 // ------------------------------------------------------------------ fused MF-Q episode
@@ -444,13 +482,16 @@ hipError_t launch_ising_mfq(const IsingMfqArgs& a, int R, hipStream_t st) {
 
 hipError_t launch_mt_words(uint32_t seed0, int r0, int R, int n_blocks, uint32_t* words, size_t stride, hipStream_t st) {
     if (R < 1 || n_blocks < 1 || stride < (size_t)n_blocks * kMtN) return hipErrorInvalidValue;
-    k_mt_words<<<(R + 3) / 4, 256, 0, st>>>(seed0, r0, R, n_blocks, words, stride);
+    k_mt_words<<<R, 256, 0, st>>>(seed0, r0, n_blocks, words, stride);
     return hipGetLastError();
 }
 
 hipError_t launch_ising_scan(const IsingScanArgs& a, int R, hipStream_t st) {
     if (a.N < 1 || a.N > kIsingMaxN || a.T < 1 || (a.n_upd < a.N && (!a.mask || !a.perm))) return hipErrorInvalidValue;
-    k_ising_scan<<<R, 64, 0, st>>>(a);
+    switch (a.ring) {                                        // the ring's blocks (A/B: MFX_ISING_SCAN_RING)
+        case 16: k_ising_scan<16><<<R, 64, 0, st>>>(a); break;
+        default: k_ising_scan<32><<<R, 64, 0, st>>>(a); break;
+    }
     return hipGetLastError();
 }
 

@@ -14,6 +14,17 @@ void set_last_error(const std::string& msg) {
     std::lock_guard<std::mutex> lk(g_err_mu);
     g_last_error = msg;
 }
+
+int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int n = 0;
+        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cache[dev];
+}
 }  // namespace mfx
 
 extern "C" {

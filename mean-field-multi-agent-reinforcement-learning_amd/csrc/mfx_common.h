@@ -17,6 +17,9 @@ namespace mfx {
 
 void set_last_error(const std::string& msg);
 
+// Compute units of the current device (256 on MI355X; 256 when the query fails), per device, cached.
+int device_cus();
+
 inline int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 inline int fail(const char* fmt, ...) {
     char buf[1024];

@@ -2,7 +2,7 @@
 
 The library is located like the reference does it -- ``<package>/../../build/libmagent.so``
 -- unless ``MAGENT_LIB`` names another build.  Because the ABI is the reference's own
-(runtime_api.h:118-181), the same binding also drives the reference engine build and the
+(runtime_api.h:20-55), the same binding also drives the reference engine build and the
 C oracle used by the tests (``load_library(path)``).
 """
 import ctypes

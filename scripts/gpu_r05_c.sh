@@ -17,5 +17,5 @@ for R in 4096 16384; do
 timeout -k 10 300 python scripts/bench_ising.py --mode reference --replicas $R --no-cpu > $O/bench_reference_$R.json 2> $O/err || { tail -20 $O/err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_reference_$R.json')); print('reference R=$R', '%.4e' % d['value'], 'call s %.4f' % d['seconds_call'], d.get('check'))"
 done
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o ising -- python3 $GRAFT_REPO_ROOT/scripts/bench_ising.py --mode reference --no-cpu > $GRAFT_REPO_ROOT/$O/bench_reference_prof.json 2> $GRAFT_REPO_ROOT/$O/prof.err || { tail -20 $GRAFT_REPO_ROOT/$O/prof.err; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o ising -- python3 $GRAFT_REPO_ROOT/scripts/bench_ising.py --mode reference --no-cpu > $GRAFT_REPO_ROOT/$O/bench_reference_prof.json 2> $GRAFT_REPO_ROOT/$O/prof.err || { tail -20 $GRAFT_REPO_ROOT/$O/prof.err; exit 1; }
 find $GRAFT_REPO_ROOT/$O/prof -name "*kernel_stats.csv" | head -3
