@@ -258,6 +258,21 @@ public:
     DevBuf<int32_t> ro_q_cnt, ro_q_left, ro_q_done;
     int ro_q_grid = 0, ro_qpar = 0;
     uint32_t ro_qlaunch = 0;                 // launches so far (item tags)
+    // Large envs on the queue kernel (not pipelined): the envs run in ro_qchunks consecutive launches per block of
+    // steps, each over one chunk of envs with queues of its own.  One launch over all envs slows past ~2048 envs at
+    // 256x256 (0.80 of the HBM roofline at 2048, 0.77 at 2560, 0.71 at 3072, 0.62-0.64 at 4096, ~0.3 MB of env state
+    // each); 4096 envs as two launches of 2048 run at 0.79, while 3072 as two of 1536 gain nothing (0.711 vs 0.714):
+    // so the chunks are at least kBigqChunkBytes of state (2048 envs at 256x256) -- floor(state / kBigqChunkBytes)
+    // of them (profiles/r05_bigq_chunks.txt).
+    static constexpr int kMaxQChunks = 8;
+    static constexpr size_t kBigqChunkBytes = (size_t)2048 * 312648;
+    int ro_qchunks = 1;
+    int ro_qc_e0[kMaxQChunks + 1] = {};
+    int ro_qc_par[kMaxQChunks] = {};
+    uint32_t ro_qc_launch[kMaxQChunks] = {};
+    State ro_qc_s[kMaxQChunks];
+    RolloutArgs ro_qc_ra[kMaxQChunks];
+    DevBuf<RolloutCtx> ro_qc_ctx;
     static uint32_t qtag(uint32_t launch) { return launch % 63u + 1u; }   // 6 tag bits (rollout_big.inc), never 0
     bool ro_prep_stale = true;               // ro_mm / ro_info / items lag the state (per-call calls since)
     DevBuf<int32_t> ro_actions, ro_eplen, ro_tx, ro_ty;
@@ -343,6 +358,33 @@ public:
         if (q.food) q.food += e0 * cn;
         q.idx_mark += e0;
         return q;
+    }
+    // The queue kernel's view of env chunk k (envs [e0, e0 + n)): every per-env array from e0, the chunk's own
+    // queue lists and counters (rollout_plan sizes them: q_list_cap per list of one chunk).
+    RolloutArgs chunk_args(int e0, int k) const {
+        RolloutArgs q = ra;
+        const int G = n_groups();
+        const size_t rc = (size_t)ra.rowcap;
+        for (int g = 0; g < G; g++) {
+            const TypeParams& T = gp.type[g];
+            q.view[g] += e0 * rc * T.view_w * T.view_h * gp.n_ch;
+            q.feat[g] += e0 * rc * gp.feat_size[g];
+        }
+        q.actions += e0 * G * rc; q.rewards += e0 * G * rc; q.mean_act += (size_t)e0 * G * ra.mean_stride;
+        q.ep_return += (size_t)e0 * G; q.ep_len += e0; q.stats += (size_t)e0 * 4; q.agent_steps += e0;
+        if (q.obs_mm) { q.obs_mm += (size_t)e0 * G * 169; q.obs_info += (size_t)e0 * s.cap; }
+        q.env_base = e0;
+        if (q.big_sort) q.big_sort += (size_t)e0 * s.acap;
+        q.q_items += (size_t)k * 2 * kXcds * ra.q_list_cap;
+        q.q_cnt += (size_t)k * 2 * kXcds * kObsCntPad;
+        q.q_left += e0; q.q_si += e0;
+        return q;
+    }
+    // Bytes of one env's state a large-env step and its observation items cycle through (cells, the per-slot arrays,
+    // the group lists, the action buffers, the observation's minimap and info words, the move sort buffer).
+    size_t env_state_bytes() const {
+        const size_t c = (size_t)s.cap, a = (size_t)s.acap, G = (size_t)n_groups();
+        return (size_t)s.cells_n * 2 + c * (4 + 4 + 4 + 4 + 1 + 4 + 1 + 2 + 4) + G * c * 2 + 3 * a * 4 + G * 169 * 4;
     }
     RolloutArgs sub_args(int e0, int k) const {
         RolloutArgs q = ra;
@@ -1276,13 +1318,28 @@ public:
                             ro_q_grid = std::min(ro_q_grid, pg);
                             ra.few_pipe = E <= ro_q_grid / 4;
                         }
+                        // env chunks (not pipelined): envs per launch by the state bytes one launch cycles through
+                        ro_qchunks = 1;
+                        if (!ra.few_pipe) {
+                            const char* qc = getenv("MFX_BIGQ_CHUNK");         // A/B and tests: envs per launch
+                            if (qc) {
+                                const long long want = atoll(qc);
+                                if (want > 0 && want < E)
+                                    ro_qchunks = (int)std::min<long long>(kMaxQChunks, (E + want - 1) / want);
+                            } else {
+                                const size_t k = (size_t)E * env_state_bytes() / kBigqChunkBytes;
+                                ro_qchunks = (int)std::max<size_t>(1, std::min<size_t>(kMaxQChunks, k));
+                            }
+                        }
+                        for (int k = 0; k <= ro_qchunks; ++k) ro_qc_e0[k] = (int)((long long)E * k / ro_qchunks);
+                        const int qmax = (E + ro_qchunks - 1) / ro_qchunks;
                         // per list and parity: one filing per env and step of a launch (<= 64 steps; the
                         // pipelined form kMaxPipeSub) (+ the tickets workgroups hold past the last filing: two
-                        // per workgroup)
-                        const size_t lcap = (size_t)((E + kXcds - 1) / kXcds) * (ra.few_pipe ? kMaxPipeSub : 64) *
+                        // per workgroup); one such set per env chunk
+                        const size_t lcap = (size_t)((qmax + kXcds - 1) / kXcds) * (ra.few_pipe ? kMaxPipeSub : 64) *
                                             (size_t)(n_groups() * chunks) + 2 * (size_t)ro_q_grid;
-                        ro_q_items.ensure(2 * kXcds * lcap);
-                        ro_q_cnt.ensure(2 * kXcds * kObsCntPad);
+                        ro_q_items.ensure(2 * kXcds * lcap * ro_qchunks);
+                        ro_q_cnt.ensure(2 * kXcds * kObsCntPad * ro_qchunks);
                         ro_q_left.ensure(E); ro_q_si.ensure(E); ro_q_done.ensure(kObsCntPad);
                         MFX_HIP_THROW(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
                         MFX_HIP_THROW(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
@@ -1354,6 +1411,20 @@ public:
             ro_ctx.ensure(1);
             ro_ctx_host.s = s; ro_ctx_host.ra = ra; ro_ctx_host.w = s;
             MFX_HIP_THROW(hipMemcpyAsync(ro_ctx.p, &ro_ctx_host, sizeof(RolloutCtx), hipMemcpyHostToDevice, stream));
+            if (ro_big && ro_bigq && !ra.few_pipe) {
+                ro_qc_ctx.ensure(ro_qchunks);
+                std::vector<RolloutCtx> qc(ro_qchunks);
+                for (int k = 0; k < ro_qchunks; ++k) {
+                    const int e0 = ro_qc_e0[k], n = ro_qc_e0[k + 1] - e0;
+                    ro_qc_s[k] = ro_qchunks > 1 ? sub_state(e0, n) : s;
+                    ro_qc_ra[k] = ro_qchunks > 1 ? chunk_args(e0, k) : ra;
+                    qc[k].s = ro_qc_s[k]; qc[k].ra = ro_qc_ra[k]; qc[k].w = ro_qc_s[k];
+                    ro_qc_par[k] = 0;
+                    ro_qc_launch[k] = ro_qlaunch;
+                }
+                MFX_HIP_THROW(hipMemcpyAsync(ro_qc_ctx.p, qc.data(), sizeof(RolloutCtx) * ro_qchunks, hipMemcpyHostToDevice,
+                                             stream));
+            }
             MFX_HIP_THROW(hipStreamSynchronize(stream));
         } catch (const HipFailure& f) {
             return fail("%s", f.what());
@@ -1410,30 +1481,42 @@ public:
                 // Re-seed after per-call calls: the last launch's filings for the next launch (never
                 // consumed) still hold the live tag in the slots past the new, smaller filing count --
                 // clear every slot and move to a fresh tag, so no stale word can pass for an item.
-                ro_qpar = 0;
 #ifndef MFX_AB_R2_RESEED                 // A/B only: the round-2 re-seed, which the regression test must catch
-                ro_qlaunch++;
                 MFX_HIP(hipMemsetAsync(ro_q_items.p, 0, ro_q_items.n * sizeof(uint32_t), stream));
 #endif
-                MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, 2 * lst * sizeof(int32_t), stream));
+                MFX_HIP(hipMemsetAsync(ro_q_cnt.p, 0, ro_q_cnt.n * sizeof(int32_t), stream));
                 MFX_HIP(hipMemsetAsync(ro_q_done.p, 0, kObsCntPad * sizeof(int32_t), stream));
-                MFX_HIP(launch_bigq_seed(d_gp, s, ra, ro_qpar, qtag(ro_qlaunch), ra.step_index, stream));
+                for (int c = 0; c < ro_qchunks; ++c) {
+                    ro_qc_par[c] = 0;
+#ifndef MFX_AB_R2_RESEED
+                    ro_qc_launch[c]++;
+#endif
+                    MFX_HIP(launch_bigq_seed(d_gp, ro_qc_s[c], ro_qc_ra[c], 0, qtag(ro_qc_launch[c]), ra.step_index,
+                                             stream));
+                }
             }
             ro_prep_stale = false;
-            for (int i = 0; i < n_steps;) {
-                const int k = std::min(sub_steps(), n_steps - i);
-                MFX_HIP(hipMemsetAsync(ro_q_cnt.p + (ro_qpar ^ 1) * lst, 0, lst * sizeof(int32_t), stream));
-                BigqSerial serial(stream);
-                MFX_HIP(serial.status());
-                MFX_HIP(launch_rollout_bigq(gp, d_gp, s, ro_ctx.p, ra.obs_item_rows, ra.step_index, k, ro_qpar,
-                                            qtag(ro_qlaunch), qtag(ro_qlaunch + 1), ro_q_grid,
-                                            ra.lds_step, stream));
-                ro_qpar ^= 1;
-                ro_qlaunch++;
-                ro_launch++;
-                ra.step_index += k;
-                i += k;
+            // chunk after chunk, each through every launch of the n steps (the envs are independent; within a
+            // chunk the launches chain as one batch's would)
+            for (int c = 0; c < ro_qchunks; ++c) {
+                int32_t* cnt = ro_q_cnt.p + (size_t)c * 2 * lst;
+                uint32_t si = ra.step_index;
+                for (int i = 0; i < n_steps;) {
+                    const int k = std::min(sub_steps(), n_steps - i);
+                    MFX_HIP(hipMemsetAsync(cnt + (ro_qc_par[c] ^ 1) * lst, 0, lst * sizeof(int32_t), stream));
+                    BigqSerial serial(stream);
+                    MFX_HIP(serial.status());
+                    MFX_HIP(launch_rollout_bigq(gp, d_gp, ro_qc_s[c], ro_qc_ctx.p + c, ra.obs_item_rows, si, k,
+                                                ro_qc_par[c], qtag(ro_qc_launch[c]), qtag(ro_qc_launch[c] + 1),
+                                                ro_q_grid, ra.lds_step, stream));
+                    ro_qc_par[c] ^= 1;
+                    ro_qc_launch[c]++;
+                    ro_launch++;
+                    si += k;
+                    i += k;
+                }
             }
+            ra.step_index += n_steps;
             return 0;
         }
         if (ro_big) {

@@ -1071,6 +1071,30 @@ def test_rollout_bigq_queue_step_one_workgroup_per_xcd(monkeypatch):
         assert torch.equal(x, y), k
 
 
+@pytest.mark.parametrize("map_size,agents,E,T,chunk", [(64, 128, 12, 432, "5"), (256, 4096, 16, 48, "6")])
+def test_rollout_bigq_env_chunks_match_one_launch(monkeypatch, map_size, agents, E, T, chunk):
+    """The queue kernel over env chunks (MFX_BIGQ_CHUNK: consecutive launches over envs [0, 4), [4, 8), ... with
+    queues of their own -- the engine's form past ~640 MB of env state) against one launch over every env, bit for
+    bit: every output buffer and the per-call state after T steps at 20 steps per launch (staggered envs)."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    left, right = bd.block_positions(map_size, agents // 2)
+    monkeypatch.setenv("MFX_FEW_PIPE", "0")
+    dumps = []
+    for ch in ("0", chunk):
+        monkeypatch.setenv("MFX_BIGQ_CHUNK", ch)
+        eng = BattleBatch(map_size, E, stream=torch.cuda.current_stream())
+        eng.rollout_init([left, right], max_steps=400, eps=0.2, seed=37, stagger=True)
+        eng.rollout_substeps(20)
+        assert eng.rollout_path() == "k_rollout_bigq"
+        eng.rollout_step(T)
+        eng.rollout_check()
+        dumps.append(_dump_rollout(eng, E, agents // 2))
+        del eng
+    for (k, x), (_, y) in zip(dumps[0], dumps[1]):
+        assert torch.equal(x, y), k
+
+
 def test_rollout_substeps_auto_choice():
     """rollout_substeps(0): the engine picks the steps per launch for its path and batch (BattleEngine::sub_steps):
     1024 for the pipelined few-env stepper (in practice the whole rollout_step), 2 for k_rollout below 96 envs per
