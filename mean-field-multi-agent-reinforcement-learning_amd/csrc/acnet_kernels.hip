@@ -50,7 +50,7 @@ constexpr int kABlocks = 19;
 // 15 wvd [544][256] MF value dense  16 bvd [256]
 // 17 wvo [256][16] MF value (column 0)                                           18 bvo [16]
 // (blocks 9-10 are empty with mean field, 11-18 without.)
-// The weight images of the GEMM layers (policy_gemm.h wg_gemm_i; made at set_weights by k_acnet_image):
+// The weight images of the GEMM layers (policy_gemm.h wg_gemm_i; made at set_weights by launch_weight_image):
 //  0 wv  1 wd0  2 wd1  3 wp (units 0..255 of d)  4 wp (units 256..511)  5 wval (0..255)  6 wval (256..511)
 //  7 wep  8 wdp  9 wvd  10 wvo
 constexpr int kAImg = 11;
@@ -59,39 +59,6 @@ struct ACNetDev {
     const float* img[kAImg];
     int V, Vp, F, Fp, A, Ap, use_mf;
 };
-
-// One weight image: thread per image float -> the source weight (zero past K and in the MT < 4 padding).
-__global__ void __launch_bounds__(256) k_acnet_image(const float* __restrict__ src, int K, int N, float* __restrict__ dst,
-                                                     size_t n) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int mt = N / 16, rw = img_row(mt);
-    const int pos = (int)(i % rw), r = (int)((i / rw) % 16);
-    const size_t ch = i / ((size_t)16 * rw);
-    int c, t;
-    if (mt % 4) {
-        c = pos / 4;
-        t = pos % 4;
-    } else {
-        const int G = mt / 4;
-        c = pos / mt;
-        const int rem = pos % mt, slot = rem / 4;
-        t = 4 * ((slot - c * G / 16 + G) % G) + rem % 4;
-    }
-    const size_t k = ch * 16 + r;
-    dst[i] = (t < mt && k < (size_t)K) ? src[k * N + 16 * t + c] : 0.f;
-}
-
-// acc[t] = bias[16 t + 4 h .. + 3] (a layer's accumulators start at its bias: one 16-B load per tile, issued
-// together, instead of one dependent load per unit after the GEMM)
-__device__ __forceinline__ void bias_init(f32x4* acc, const float* bias, int h) {
-    const float4* b = reinterpret_cast<const float4*>(bias) + h;
-    float4 v[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) v[t] = b[4 * t];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) acc[t] = {v[t].x, v[t].y, v[t].z, v[t].w};
-}
 
 // x / 0.1f, correctly rounded (the reference's dense / 0.1): q = x * 10, one fma residual and one fma correction --
 // equal to the IEEE quotient for every f32 |x| >= 2^-100 (checked exhaustively, scripts/micro/div_tenth.c); tinier
@@ -384,7 +351,7 @@ struct ACNetHandle {
     ACNetDev dev{};
     float* blob = nullptr;
     size_t blob_n = 0;
-    float* img = nullptr;                 // the weight images (k_acnet_image), made by set_weights
+    float* img = nullptr;                 // the weight images (launch_weight_image), made by set_weights
     size_t img_n = 0;
     bool imaged = false;
 };
@@ -472,9 +439,9 @@ MFX_API int mfx_acnet_set_weights(void* handle, const float* d_blob, size_t n_fl
     for (int k = 0; k < kAImg; ++k) {
         if (!im[k].K) continue;
         const size_t n = img_floats(im[k].K, im[k].N / 16);
-        k_acnet_image<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-            q->dev.w[im[k].block] + (size_t)im[k].row0 * im[k].N, im[k].K, im[k].N, const_cast<float*>(q->dev.img[k]), n);
-        MFX_HIP(hipGetLastError());
+        (void)n;
+        MFX_HIP(launch_weight_image(q->dev.w[im[k].block] + (size_t)im[k].row0 * im[k].N, im[k].K, im[k].N,
+                                    const_cast<float*>(q->dev.img[k]), (hipStream_t)stream));
     }
     q->imaged = true;
     return 0;

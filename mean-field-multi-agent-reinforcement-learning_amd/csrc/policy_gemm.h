@@ -231,6 +231,21 @@ __device__ __forceinline__ void wg_gemm_i(const float* __restrict__ img, int K, 
     }
 }
 
+// acc[t] = bias[16 t + 4 h .. + 3] (a layer's accumulators start at its bias: one 16-B load per tile, issued
+// together, instead of one dependent load per unit after the GEMM)
+__device__ __forceinline__ void bias_init(f32x4* acc, const float* bias, int h) {
+    const float4* b = reinterpret_cast<const float4*>(bias) + h;
+    float4 v[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v[t] = b[4 * t];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = {v[t].x, v[t].y, v[t].z, v[t].w};
+}
+
+// The image (img_row / img_pos layout above) of a [K][N] row-major weight matrix into dst (img_floats(K, N / 16)
+// floats): one thread per image float, zero past K and in the MT < 4 padding (policy_kernels.hip k_weight_image).
+hipError_t launch_weight_image(const float* src, int K, int N, float* dst, hipStream_t st);
+
 // relu(acc + bias) of unit 16 t + 4 h + s: the B operand of the next layer's chunk t, k-step s.
 __device__ __forceinline__ float relu_unit(const f32x4* acc, const float* __restrict__ bias, int t, int s) {
     const int h = (tid_x() & 63) >> 4;

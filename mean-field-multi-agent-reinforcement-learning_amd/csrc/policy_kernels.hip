@@ -14,14 +14,15 @@
 // (157 TF/s -> ~4.6e7 agents/s for the whole chip).  Two kernels:
 //   k_qnet_conv  one wave per agent: the view staged in LDS, Conv1 as an implicit GEMM over 121
 //                positions x 32 channels x K 63 (padded to 64), its output kept in LDS, Conv2 as an
-//                implicit GEMM over 81 positions x 32 x K 288 (16-B operand reads, k permuted inside each
-//                (ky, kx) block); the 2,592 activations to HBM (10 KB/agent)
+//                implicit GEMM over 80 positions x 32 x K 288 (16-B operand reads, k permuted inside each
+//                (ky, kx) block) and its 81st position on the VALU; the 2,592 activations to HBM (10 KB/agent)
 //   k_qnet_head  four waves x 16 agents per workgroup: every layer transposed (weights as the A operand),
 //                so each layer's accumulators are the next layer's B operand in registers; the weight
 //                chunks staged in LDS and shared by the four waves; the Q values and the argmax
 // A and B operands of v_mfma_f32_16x16x4_f32: lane l holds A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15];
 // D: lane l holds D[(l >> 4) * 4 + r][l & 15], r = 0..3 (cdna_hip_programming.md, fragment layout).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -46,7 +47,37 @@ constexpr int kQHObs = 256, kQHEmb = 32, kQHP1 = 64, kQHP2 = 32, kQH2 = 128, kQH
 struct QNetDev {
     const float *w1, *b1, *w2, *b2, *wd, *bd, *we, *be, *wp1, *bp1, *wp2, *bp2, *w2d, *b2d, *wo, *bo, *wq, *bq;
     int F, Fp, A, Ap, use_mf, Kc;   // Kc: Dense2 input width (288, or 320 with mean field)
+    const float* wd_img;            // Dense-Obs's weight image (policy_gemm.h wg_gemm_i), made by set_weights
 };
+
+// One weight image: thread per image float -> the source weight (zero past K and in the MT < 4 padding).
+__global__ void __launch_bounds__(256) k_weight_image(const float* __restrict__ src, int K, int N, float* __restrict__ dst,
+                                                      size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int mt = N / 16, rw = img_row(mt);
+    const int pos = (int)(i % rw), r = (int)((i / rw) % 16);
+    const size_t ch = i / ((size_t)16 * rw);
+    int c, t;
+    if (mt % 4) {
+        c = pos / 4;
+        t = pos % 4;
+    } else {
+        const int G = mt / 4;
+        c = pos / mt;
+        const int rem = pos % mt, slot = rem / 4;
+        t = 4 * ((slot - c * G / 16 + G) % G) + rem % 4;
+    }
+    const size_t k = ch * 16 + r;
+    dst[i] = (t < mt && k < (size_t)K) ? src[k * N + 16 * t + c] : 0.f;
+}
+
+hipError_t launch_weight_image(const float* src, int K, int N, float* dst, hipStream_t st) {
+    if (K < 1 || N < 16 || N % 16 || N / 16 > kQMaxMT) return hipErrorInvalidValue;
+    const size_t n = img_floats(K, N / 16);
+    k_weight_image<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(src, K, N, dst, n);
+    return hipGetLastError();
+}
 
 
 // ------------------------------------------------------------------------------------------ conv
@@ -137,23 +168,26 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
             }
         }
         qwave_sync();
-        // ---- Conv2: 6 position tiles (81 of 96 rows) x 2 channel tiles, K 288 = 9 (ky, kx) blocks x 32 ci.
-        // Inside block b the 8 k-steps j give lane group h the channels ci = 8 h + j (any order of k is the same
-        // sum up to rounding), so a lane's A operands of a block (per tile) and B operands (per channel tile) are
-        // 8 consecutive floats: 16 ds_read_b128 per block for 96 MFMAs, the next block's in flight meanwhile.
-        f32x4 acc[6][2];
-        int cb[6];
+        // ---- Conv2: 5 position tiles (positions 0-79) x 2 channel tiles on the MFMA, K 288 = 9 (ky, kx) blocks x
+        // 32 ci, and position 80 -- the 81st, which a sixth tile would carry with 15 rows of padding (16 % more MFMA
+        // work) -- on the VALU below.  Inside block b the 8 k-steps j give lane group h the channels ci = 8 h + j
+        // (any order of k is the same sum up to rounding), so a lane's A operands of a block (per tile) and B
+        // operands (per channel tile) are 8 consecutive floats: 14 ds_read_b128 per block for 80 MFMAs, the next
+        // block's in flight meanwhile.
+        constexpr int kMT2 = 5;
+        f32x4 acc[kMT2][2];
+        int cb[kMT2];
 #pragma unroll
-        for (int mt = 0; mt < 6; ++mt) {
-            const int pa = min(mt * 16 + c, kQC2 * kQC2 - 1);
+        for (int mt = 0; mt < kMT2; ++mt) {
+            const int pa = mt * 16 + c;
             cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQC1Ld + 8 * h;
             acc[mt][0] = {0.f, 0.f, 0.f, 0.f};
             acc[mt][1] = {0.f, 0.f, 0.f, 0.f};
         }
         typedef float f32x8 __attribute__((ext_vector_type(8)));
-        // Each block's 16 reads go out in two parts under the previous block's MFMAs (10 before its first half,
-        // 6 before its second), so no wait ever has to name more than 15 newer LDS operations (lgkmcnt's range).
-        f32x8 p0[6], q0[2], p1[6], q1[2];
+        // Each block's 14 reads go out in two parts under the previous block's MFMAs (9 before its first half,
+        // 5 before its second), so no wait ever has to name more than 15 newer LDS operations (lgkmcnt's range).
+        f32x8 p0[kMT2], q0[2], p1[kMT2], q1[2];
         auto conv2_part = [&](int b, f32x8* a, f32x8* w, int part) {
             const int ky = b / 3, kx = b % 3;
             const int so = (ky * kQC1 + kx) * kQC1Ld;
@@ -164,14 +198,14 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
                 for (int mt = 0; mt < 3; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
             } else {
 #pragma unroll
-                for (int mt = 3; mt < 6; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
+                for (int mt = 3; mt < kMT2; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
             }
         };
         auto conv2_half = [&](const f32x8* a, const f32x8* w, int j0) {
 #pragma unroll
             for (int j = j0; j < j0 + 4; ++j)
 #pragma unroll
-                for (int mt = 0; mt < 6; ++mt) {
+                for (int mt = 0; mt < kMT2; ++mt) {
                     acc[mt][0] = mfma4(a[mt][j], w[0][j], acc[mt][0]);
                     acc[mt][1] = mfma4(a[mt][j], w[1][j], acc[mt][1]);
                 }
@@ -197,22 +231,44 @@ __global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __
         conv2_step(p0, q0, p1, q1, -1);                  // block 8
         float* o = out + (size_t)i * kQFlat;
 #pragma unroll
-        for (int mt = 0; mt < 6; ++mt)
+        for (int mt = 0; mt < kMT2; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int pos = mt * 16 + h * 4 + r;
-                if (pos < kQC2 * kQC2) {
-                    o[pos * kQCh + c] = fmaxf(acc[mt][0][r] + bias2a, 0.f);
-                    o[pos * kQCh + 16 + c] = fmaxf(acc[mt][1][r] + bias2b, 0.f);
-                }
+                o[pos * kQCh + c] = fmaxf(acc[mt][0][r] + bias2a, 0.f);
+                o[pos * kQCh + 16 + c] = fmaxf(acc[mt][1][r] + bias2b, 0.f);
             }
+        {
+            // position 80 (row 8, column 8) on the VALU: lane l sums output channel l % 32 over half l / 32 of
+            // the 288 k (blocks 0-3 and half of 4 / the rest), 16-B reads of the patch (broadcast) and of w2t
+            const int co = lane & 31, k0 = (lane >> 5) * 144;
+            const float4* wr = reinterpret_cast<const float4*>(w2 + co * kQW2tLd + k0);
+            float sum = 0.f;
+#pragma unroll 4
+            for (int q = 0; q < 36; ++q) {
+                const int k = k0 + 4 * q, b = k >> 5, ci = k & 31;
+                const float4 x = *reinterpret_cast<const float4*>(c1 + ((8 + b / 3) * kQC1 + 8 + b % 3) * kQC1Ld + ci);
+                const float4 w = wr[q];
+                sum = __builtin_fmaf(x.x, w.x, sum);
+                sum = __builtin_fmaf(x.y, w.y, sum);
+                sum = __builtin_fmaf(x.z, w.z, sum);
+                sum = __builtin_fmaf(x.w, w.w, sum);
+            }
+            sum += __shfl_xor(sum, 32);
+            if (lane < 32) o[80 * kQCh + co] = fmaxf(sum + p.b2[co], 0.f);
+        }
         qwave_sync();                                    // vs / c1 are rewritten by the next agent
     }
 }
 
 // ------------------------------------------------------------------------------------------ head
 
-template <typename PT>
+// kImg (the default): Dense-Obs over its weight image (wg_gemm_i, direct-to-LDS chunks) with the conv activations
+// through an LDS ring filled two chunks ahead, its accumulators starting at the bias; else the register-staged
+// wg_gemm_t (A/B: MFX_QNET_IMG=0).  LDS: the image path's 32 KB of chunks + the 12 KB ring, then the small layers'
+// wg_gemm_t staging from offset 0.
+constexpr size_t kQHeadImgSmem = kImgSmem + 3 * 1024 * 4 > kQHeadSmem ? kImgSmem + 3 * 1024 * 4 : kQHeadSmem;
+template <typename PT, bool kImg>
 __global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __restrict__ conv, int n,
                                                       const float* __restrict__ feat, size_t feat_ld,
                                                       const PT* __restrict__ prob, size_t prob_ld, QRowMap rm,
@@ -229,7 +285,36 @@ __global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __
     const int env = rm.rows ? row / rm.rowcap : ia;
     // ---- Dense-Obs^T [256 x 16]: the conv activations of this lane's agent, 4 consecutive per chunk step
     f32x4 hobs[16];
-    {
+    if constexpr (kImg) {
+        // the activation rows through LDS: a ring of 3 chunks (64 agents x 16 floats each), filled two chunks ahead
+        // by direct-to-LDS loads -- instruction q of wave w: agent 4 (4 w + q) + lane / 16, float lane % 16
+        float* ring = bsm + 2 * kImgBuf;
+        const float* src[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            src[q] = conv + (size_t)min((int)blockIdx.x * kQHeadWaves * 16 + 4 * (4 * wid + q) + (lane >> 4), n - 1) * kQFlat;
+        auto ring_issue = [&](int ch) {
+            float* dst = ring + (ch % 3) * 1024 + wid * 256;
+            const int k = min(16 * ch + c, kQFlat - 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_global_load_lds((const void*)(src[q] + k),
+                                                 (__attribute__((address_space(3))) void*)(dst + q * 64), 4, 0, 0);
+        };
+        ring_issue(0);
+        ring_issue(1);
+        float4 xv;
+        auto vat = [&](int ch, int s) {
+            if (s == 0) xv = reinterpret_cast<const float4*>(ring + (ch % 3) * 1024)[(16 * wid + c) * 4 + h];
+            return s == 0 ? xv.x : s == 1 ? xv.y : s == 2 ? xv.z : xv.w;
+        };
+        bias_init(hobs, p.bd, h);
+        wg_gemm_i<16, 0, false, 4>(p.wd_img, kQFlat, vat, bsm, hobs, [&](int ch) { ring_issue(ch + 2); });
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hobs[t][r] = fmaxf(hobs[t][r], 0.f);
+    } else {
         const float4* ar = reinterpret_cast<const float4*>(conv + (size_t)ia * kQFlat) + h;   // k = 16 ch + 4 h + s
         float4 cur4 = ar[0], nxt4 = cur4;
         int have = 0;
@@ -264,7 +349,7 @@ __global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __
     // 16-17 h_emb, 18-19 h_prob
     f32x4 d2[8];
     wg_gemm_t<8, (kQHObs + kQHEmb + kQHP2) / 16>(p.w2d, p.Kc, [&](int ch, int s) {
-        if (ch < 16) return relu_unit(hobs, p.bd, ch, s);
+        if (ch < 16) return kImg ? hobs[ch][s] : relu_unit(hobs, p.bd, ch, s);   // (kImg: activated in place)
         if (ch < 18) return relu_unit(hemb, p.be, ch - 16, s);
         return relu_unit(hp, p.bp2, ch - 18, s);
     }, bsm, d2);
@@ -346,6 +431,8 @@ struct QNetHandle {
     float* blob = nullptr;
     size_t blob_n = 0;
     DevBuf<float> conv;           // [n][2592] activations between the kernels
+    float* img = nullptr;         // Dense-Obs's weight image (made by set_weights)
+    bool imaged = false;
 };
 
 // Offsets (floats) of every matrix / bias in the packed blob, in the order of QNetDev.
@@ -390,6 +477,12 @@ MFX_API int mfx_qnet_create(int view_h, int view_w, int n_ch, int feature, int n
                            &q->dev.bo, &q->dev.wq, &q->dev.bq};
     for (int k = 0; k < 18; ++k) *f[k] = q->blob + off[k];
     q->dev.F = feature; q->dev.Fp = Fp; q->dev.A = n_action; q->dev.Ap = Ap; q->dev.use_mf = use_mf; q->dev.Kc = Kc;
+    if (hipMalloc(&q->img, img_floats(kQFlat, kQHObs / 16) * sizeof(float)) != hipSuccess) {
+        (void)hipFree(q->blob);
+        delete q;
+        return fail("qnet: hipMalloc of the Dense-Obs image");
+    }
+    q->dev.wd_img = q->img;
     *handle = q;
     return 0;
 }
@@ -398,6 +491,7 @@ MFX_API int mfx_qnet_destroy(void* handle) {
     auto* q = static_cast<QNetHandle*>(handle);
     if (!q) return 0;
     if (q->blob) (void)hipFree(q->blob);
+    if (q->img) (void)hipFree(q->img);
     delete q;
     return 0;
 }
@@ -407,6 +501,8 @@ MFX_API int mfx_qnet_set_weights(void* handle, const float* d_blob, size_t n_flo
     auto* q = static_cast<QNetHandle*>(handle);
     if (n_floats != q->blob_n) return fail("qnet_set_weights: %zu floats, the layout has %zu", n_floats, q->blob_n);
     MFX_HIP(hipMemcpyAsync(q->blob, d_blob, n_floats * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    MFX_HIP(launch_weight_image(q->dev.wd, kQFlat, kQHObs, q->img, (hipStream_t)stream));
+    q->imaged = true;
     return 0;
 }
 
@@ -440,14 +536,14 @@ static int qnet_run(QNetHandle* q, const float* view, size_t view_ld, const floa
         k_qnet_conv<<<cgrid, 256, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p, d_n, off);
         MFX_HIP(hipGetLastError());
         const int hgrid = (m + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
-        if (prob_f64)
-            k_qnet_head<double><<<hgrid, 256, kQHeadSmem, st>>>(q->dev, q->conv.p, m, f, feat_ld,
-                                                                 static_cast<const double*>(pb), prob_ld, r, qo, ao,
-                                                                 d_n, off);
-        else
-            k_qnet_head<float><<<hgrid, 256, kQHeadSmem, st>>>(q->dev, q->conv.p, m, f, feat_ld,
-                                                                static_cast<const float*>(pb), prob_ld, r, qo, ao,
-                                                                d_n, off);
+        const char* iv = getenv("MFX_QNET_IMG");                   // A/B only: 0 = wg_gemm_t's register staging
+        const bool img = q->imaged && !(iv && atoi(iv) == 0);
+#define MFX_QHEAD(PT, IMG)                                                                                         \
+        k_qnet_head<PT, IMG><<<hgrid, 256, IMG ? kQHeadImgSmem : kQHeadSmem, st>>>(                                  \
+            q->dev, q->conv.p, m, f, feat_ld, static_cast<const PT*>(pb), prob_ld, r, qo, ao, d_n, off)
+        if (prob_f64) { if (img) MFX_QHEAD(double, true); else MFX_QHEAD(double, false); }
+        else { if (img) MFX_QHEAD(float, true); else MFX_QHEAD(float, false); }
+#undef MFX_QHEAD
         MFX_HIP(hipGetLastError());
     }
     return 0;
