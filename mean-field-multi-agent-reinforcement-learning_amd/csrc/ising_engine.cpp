@@ -26,11 +26,26 @@ struct IsingEngine {
     DevBuf<double> reward, order, q, u, order_t;
     DevBuf<uint32_t> mask;
     DevBuf<int32_t> nup_t;
-    DevBuf<uint32_t> words, off[2];          // the device stream (mfx_ising_mfq_run_stream)
-    DevBuf<uint16_t> perm;
     DevBuf<int32_t> err;
     DevBuf<unsigned long long> scan_stats;   // MFX_ISING_SCAN_STATS diagnostics
-    ~IsingEngine() { if (stream) (void)hipStreamDestroy(stream); }
+    // mfx_ising_mfq_run_stream's two pass slots: pass p's words are generated and walked (gen stream) into slot
+    // p % 2 while pass p - 1's episode runs out of the other (stream)
+    struct Slot {
+        DevBuf<uint32_t> words, off[2], mask;
+        DevBuf<uint16_t> perm;
+        DevBuf<double> q, order_t;
+        DevBuf<int32_t> nup_t, steps;
+        hipEvent_t produced = nullptr, consumed = nullptr;
+    } slot[2];
+    hipStream_t gen = nullptr;
+    ~IsingEngine() {
+        for (auto& sl : slot) {
+            if (sl.produced) (void)hipEventDestroy(sl.produced);
+            if (sl.consumed) (void)hipEventDestroy(sl.consumed);
+        }
+        if (gen) (void)hipStreamDestroy(gen);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
 };
 
 }  // namespace mfx
@@ -162,18 +177,38 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
     const size_t per = (size_t)N + (size_t)episodes * ((size_t)N + (size_t)T * 4 * N) + 320;
     const int blocks = (int)((per + 623) / 624);
     const size_t W = (size_t)blocks * 624;
-    // replicas per pass: the word streams within ~16 GB
-    const int Rb = (int)std::max<size_t>(1, std::min<size_t>((size_t)R, ((size_t)16 << 30) / (W * 4)));
+    // replicas per pass: a slot's word streams within 64 GB and a third of the free memory.  Big passes: the walk
+    // is one latency-bound wave per replica, so a pass's walk takes about as long whatever its replicas -- 16384
+    // replicas at 2000 steps: 3.41e10 spin-steps/s in 16-GB passes, 3.86e10 in 64-GB ones (MFX_ISING_PASS_GB: A/B only)
+    const char* pg = getenv("MFX_ISING_PASS_GB");
+    size_t pass_bytes = (size_t)64 << 30;
+    {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr / 3 < pass_bytes) pass_bytes = std::max<size_t>(fr / 3, (size_t)1 << 30);
+    }
+    if (pg) pass_bytes = (size_t)std::max(1, atoi(pg)) << 30;
+    const int Rb = (int)std::max<size_t>(1, std::min<size_t>((size_t)R, pass_bytes / (W * 4)));
+    const int P = (R + Rb - 1) / Rb;                           // passes
     const size_t QR = (size_t)N * (K + 1) * 2;
     try {
-        e->words.ensure((size_t)Rb * W);
-        for (auto& o : e->off) o.ensure((size_t)Rb * (T + 1));
+        for (int k = 0; k < std::min(P, 2); ++k) {
+            auto& sl = e->slot[k];
+            sl.words.ensure((size_t)Rb * W);
+            for (auto& o : sl.off) o.ensure((size_t)Rb * (T + 1));
+            if (n_upd < N) { sl.perm.ensure((size_t)Rb * N); sl.mask.ensure((size_t)Rb * T * mw); }
+            sl.q.ensure((size_t)Rb * QR);
+            sl.order_t.ensure((size_t)Rb * T);
+            sl.nup_t.ensure((size_t)Rb * T);
+            sl.steps.ensure(Rb);
+            if (!sl.produced) MFX_HIP_THROW(hipEventCreateWithFlags(&sl.produced, hipEventDisableTiming));
+            if (!sl.consumed) MFX_HIP_THROW(hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming));
+        }
+        if (!e->gen) {
+            const char* gp = getenv("MFX_ISING_GEN_PRIO");           // A/B only: the gen stream's priority
+            if (gp) MFX_HIP_THROW(hipStreamCreateWithPriority(&e->gen, hipStreamNonBlocking, atoi(gp)));
+            else MFX_HIP_THROW(hipStreamCreateWithFlags(&e->gen, hipStreamNonBlocking));
+        }
         e->err.ensure(1);
-        if (n_upd < N) { e->perm.ensure((size_t)Rb * N); e->mask.ensure((size_t)Rb * T * mw); }
-        e->q.ensure((size_t)Rb * QR);
-        e->order_t.ensure((size_t)Rb * T);
-        e->nup_t.ensure((size_t)Rb * T);
-        e->steps.ensure(Rb);
         e->spins_out.ensure((size_t)R * N);
     } catch (const std::exception& ex) {
         return mfx::fail("%s", ex.what());
@@ -185,44 +220,68 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
         try { e->scan_stats.ensure(4); } catch (const std::exception& ex) { return mfx::fail("%s", ex.what()); }
         MFX_HIP(hipMemsetAsync(e->scan_stats.p, 0, 4 * sizeof(unsigned long long), e->stream));
     }
-    for (int r0 = 0; r0 < R; r0 += Rb) {
-        const int nr = std::min(Rb, R - r0);
-        MFX_HIP(mfx::launch_mt_words(seed0, r0, nr, blocks, e->words.p, W, e->stream));
+    const char* rb = getenv("MFX_ISING_SCAN_RING");                  // A/B only: 16 / 24 / 32 blocks
+    const int ring = rb ? atoi(rb) : 24;                             // (24: 3.41e10 vs 3.32e10 with 32, 16384 replicas)
+    const char* ov = getenv("MFX_ISING_OVERLAP");                    // A/B only: 0 = one stream
+    hipStream_t gs = ov && atoi(ov) == 0 ? e->stream : e->gen;
+    {   // the gen stream starts after the error word is cleared
+        hipEvent_t ready = e->slot[0].consumed;
+        MFX_HIP(hipEventRecord(ready, e->stream));
+        MFX_HIP(hipStreamWaitEvent(e->gen, ready, 0));
+    }
+    auto scan = [&](IsingEngine::Slot& sl, int r0, int nr, int ep, hipStream_t st) -> hipError_t {
+        mfx::IsingScanArgs sa{};
+        sa.N = N; sa.T = T; sa.n_upd = n_upd; sa.words = sl.words.p; sa.wstride = W;
+        sa.prev_off = ep ? sl.off[(ep - 1) & 1].p : nullptr;
+        sa.prev_steps = ep ? sl.steps.p : nullptr;
+        sa.spins0 = e->spins.p + (size_t)r0 * N;
+        sa.off = sl.off[ep & 1].p;
+        sa.mask = n_upd < N ? sl.mask.p : nullptr;
+        sa.perm = n_upd < N ? sl.perm.p : nullptr;
+        sa.err = e->err.p;
+        sa.stats = want_stats ? e->scan_stats.p : nullptr;
+        sa.ring = ring;
+        return mfx::launch_ising_scan(sa, nr, st);
+    };
+    // pass p's generation and first walk (gen stream), into slot p % 2 once pass p - 2 has released it
+    auto produce = [&](int p) -> hipError_t {
+        auto& sl = e->slot[p & 1];
+        const int r0 = p * Rb, nr = std::min(Rb, R - r0);
+        hipError_t err;
+        if (p >= 2 && (err = hipStreamWaitEvent(gs, sl.consumed, 0)) != hipSuccess) return err;
+        if ((err = mfx::launch_mt_words(seed0, r0, nr, blocks, sl.words.p, W, gs)) != hipSuccess) return err;
+        if ((err = scan(sl, r0, nr, 0, gs)) != hipSuccess) return err;
+        return hipEventRecord(sl.produced, gs);
+    };
+    MFX_HIP(produce(0));
+    if (P > 1) MFX_HIP(produce(1));
+    for (int p = 0; p < P; ++p) {
+        auto& sl = e->slot[p & 1];
+        const int r0 = p * Rb, nr = std::min(Rb, R - r0);
+        MFX_HIP(hipStreamWaitEvent(e->stream, sl.produced, 0));
         for (int ep = 0; ep < episodes; ++ep) {
-            mfx::IsingScanArgs sa{};
-            sa.N = N; sa.T = T; sa.n_upd = n_upd; sa.words = e->words.p; sa.wstride = W;
-            sa.prev_off = ep ? e->off[(ep - 1) & 1].p : nullptr;
-            sa.prev_steps = ep ? e->steps.p : nullptr;
-            sa.spins0 = e->spins.p + (size_t)r0 * N;
-            sa.off = e->off[ep & 1].p;
-            sa.mask = n_upd < N ? e->mask.p : nullptr;
-            sa.perm = n_upd < N ? e->perm.p : nullptr;
-            sa.err = e->err.p;
-            sa.stats = want_stats ? e->scan_stats.p : nullptr;
-            {
-                const char* rb = getenv("MFX_ISING_SCAN_RING");              // A/B only: 16 / 32 blocks
-                sa.ring = rb ? atoi(rb) : 32;
-            }
-            MFX_HIP(mfx::launch_ising_scan(sa, nr, e->stream));
+            if (ep) MFX_HIP(scan(sl, r0, nr, ep, e->stream));       // (after the previous episode's early stop)
             mfx::IsingMfqArgs a{};
             a.N = N; a.K = K; a.T = T; a.nbr = e->nbr.p; a.spins0 = e->spins.p + (size_t)r0 * N;
-            a.words = e->words.p; a.woff = e->off[ep & 1].p; a.wstride = W;
-            a.mask = n_upd < N ? e->mask.p : nullptr;
+            a.words = sl.words.p; a.woff = sl.off[ep & 1].p; a.wstride = W;
+            a.mask = n_upd < N ? sl.mask.p : nullptr;
             a.temperature = temperature; a.lr = lr; a.decay_rate = decay_rate; a.decay_gap = decay_gap;
-            a.q_out = e->q.p; a.order_out = e->order_t.p; a.nup_out = e->nup_t.p;
-            a.spins_out = e->spins_out.p + (size_t)r0 * N; a.steps_out = e->steps.p;
+            a.q_out = sl.q.p; a.order_out = sl.order_t.p; a.nup_out = sl.nup_t.p;
+            a.spins_out = e->spins_out.p + (size_t)r0 * N; a.steps_out = sl.steps.p;
             MFX_HIP(mfx::launch_ising_mfq(a, nr, e->stream));
             const size_t er = (size_t)ep * R + r0;               // this pass's rows of episode ep's outputs
-            MFX_HIP(hipMemcpyAsync(q + er * QR, e->q.p, sizeof(double) * nr * QR, hipMemcpyDeviceToHost, e->stream));
+            MFX_HIP(hipMemcpyAsync(q + er * QR, sl.q.p, sizeof(double) * nr * QR, hipMemcpyDeviceToHost, e->stream));
             if (order)
-                MFX_HIP(hipMemcpyAsync(order + er * T, e->order_t.p, sizeof(double) * nr * T, hipMemcpyDeviceToHost,
+                MFX_HIP(hipMemcpyAsync(order + er * T, sl.order_t.p, sizeof(double) * nr * T, hipMemcpyDeviceToHost,
                                        e->stream));
             if (n_up)
-                MFX_HIP(hipMemcpyAsync(n_up + er * T, e->nup_t.p, sizeof(int32_t) * nr * T, hipMemcpyDeviceToHost,
+                MFX_HIP(hipMemcpyAsync(n_up + er * T, sl.nup_t.p, sizeof(int32_t) * nr * T, hipMemcpyDeviceToHost,
                                        e->stream));
             if (steps)
-                MFX_HIP(hipMemcpyAsync(steps + er, e->steps.p, sizeof(int32_t) * nr, hipMemcpyDeviceToHost, e->stream));
+                MFX_HIP(hipMemcpyAsync(steps + er, sl.steps.p, sizeof(int32_t) * nr, hipMemcpyDeviceToHost, e->stream));
         }
+        MFX_HIP(hipEventRecord(sl.consumed, e->stream));
+        if (p + 2 < P) MFX_HIP(produce(p + 2));
     }
     MFX_HIP(hipMemcpyAsync(e->spins.p, e->spins_out.p, (size_t)R * N, hipMemcpyDeviceToDevice, e->stream));
     int32_t err = 0;

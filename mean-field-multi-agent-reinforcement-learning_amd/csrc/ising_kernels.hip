@@ -161,7 +161,8 @@ __global__ void __launch_bounds__(256) k_mt_words(uint32_t seed0, int r0, int n_
 // The permutation's words come from an LDS ring of RB blocks of 64 words (the uniforms are never fetched: k_ising_mfq
 // reads them): each step's blocks are fetched by direct-to-LDS loads (global_load_lds) while the step before walks.
 // The ring is the kernel's occupancy -- one wave per replica, latency-bound, so the waves per CU are its rate: RB = 32
-// (8 KB, 20 waves per CU) holds a step and the next at N = 400; words outside the ring are read from memory.
+// (8 KB, 20 waves per CU) holds a step and the next at N = 400; RB = 24 (6 KB, 26 waves) holds the step and most of
+// the next, and is the faster (+3 % at 16384 replicas); words outside the ring are read from memory.
 template <int RB>
 __global__ void __launch_bounds__(64) k_ising_scan(IsingScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[RB * 64];
@@ -490,7 +491,9 @@ hipError_t launch_ising_scan(const IsingScanArgs& a, int R, hipStream_t st) {
     if (a.N < 1 || a.N > kIsingMaxN || a.T < 1 || (a.n_upd < a.N && (!a.mask || !a.perm))) return hipErrorInvalidValue;
     switch (a.ring) {                                        // the ring's blocks (A/B: MFX_ISING_SCAN_RING)
         case 16: k_ising_scan<16><<<R, 64, 0, st>>>(a); break;
-        default: k_ising_scan<32><<<R, 64, 0, st>>>(a); break;
+        case 24: k_ising_scan<24><<<R, 64, 0, st>>>(a); break;
+        case 32: k_ising_scan<32><<<R, 64, 0, st>>>(a); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
