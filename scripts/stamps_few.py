@@ -25,6 +25,7 @@ ap.add_argument("--map", type=int, default=64)
 ap.add_argument("--agents", type=int, default=256)
 ap.add_argument("--sub", type=int, default=20)
 ap.add_argument("--launches", type=int, default=40)
+ap.add_argument("--snap", action="store_true", help="also the snapshot's sub-phases (slots 24-27)")
 a = ap.parse_args()
 # slot order along one step: snapshot, wait + file, then few_env_step (agent_phase's team stamps, the episode end)
 order = [20, 21, 22, 4, 5, 17, 18, 15, 19, 6, 7, 8, 13]
@@ -38,7 +39,7 @@ buf = torch.zeros(a.envs * a.sub * 32, dtype=torch.int64, device="cuda")
 assert eng._dll.mfx_battle_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
 eng.rollout_step(200)
 torch.cuda.synchronize()
-acc, skipped, agents, real, gaps = [], 0, [], [], []
+acc, skipped, agents, real, gaps, snap_rows = [], 0, [], [], [], []
 for t in range(a.launches):
     buf.zero_()
     eng.rollout_step(a.sub)
@@ -46,6 +47,7 @@ for t in range(a.launches):
     raw3 = buf.view(a.sub, a.envs, 32).cpu().numpy().astype(np.int64)
     gaps.append((raw3[1:, :, 30] - raw3[:-1, :, 31]).ravel())     # real-time ticks between a step's end and the next
     raw = raw3.reshape(a.sub * a.envs, 32)
+    snap_rows.append(raw.copy())
     st = raw[:, order]
     ok = (st > 0).all(1)                 # rows whose every stamp ran (moves in parallel, pipelined stepper)
     skipped += int((~ok).sum())
@@ -66,6 +68,20 @@ print("pipelined stepper, %d envs of %dx%d, %d agents, every step of %d-step lau
 for i, n in enumerate(names):
     print("%-24s median %8d  mean %8d  share %5.1f%%" % (n, np.median(d[:, i]), d[:, i].mean(),
                                                          100 * d[:, i].mean() / tot.mean()))
+if a.snap:
+    # the snapshot's sub-phases (slots 24-27, the first copying lane's clock, no barriers): from the step's start
+    # (slot 20) to the copy's start, the cells, the id arrays and lists, the minimap counts + info words, then the
+    # barrier's exit (slot 21)
+    R = np.concatenate(snap_rows)
+    sel = (R[:, 16] <= 64) & (R[:, [20, 24, 25, 26, 27, 21]] > 0).all(1)
+    q = np.diff(R[sel][:, [20, 24, 25, 26, 27, 21]], axis=1)
+    print("snapshot split (<= 64 agents, %d env-steps), medians: to copy start %d, copies %d, (none) %d, "
+          "counts+info %d, barrier %d" % ((int(sel.sum()),) + tuple(int(x) for x in np.median(q, 0))))
+    # the policy phase of the wave team (slots 22 -> 23 -> 28 -> 4): prologue + ahist zero, the policy loop, the mean
+    sel = (R[:, 16] <= 64) & (R[:, [22, 23, 28, 4]] > 0).all(1)
+    q = np.diff(R[sel][:, [22, 23, 28, 4]], axis=1)
+    print("policy split (<= 64 agents, %d env-steps), medians: prologue %d, policy loop %d, mean action %d"
+          % ((int(sel.sum()),) + tuple(int(x) for x in np.median(q, 0))))
 for lab, m in (("<= 64 agents", nag <= 64), ("65-128 agents", (nag > 64) & (nag <= 128)), ("> 128 agents", nag > 128)):
     if m.any():
         print("%s: %d env-steps, median %d cycles per step; phase medians %s" % (
