@@ -77,11 +77,13 @@ if a.snap:
     q = np.diff(R[sel][:, [20, 24, 25, 26, 27, 21]], axis=1)
     print("snapshot split (<= 64 agents, %d env-steps), medians: to copy start %d, copies %d, (none) %d, "
           "counts+info %d, barrier %d" % ((int(sel.sum()),) + tuple(int(x) for x in np.median(q, 0))))
-    # the policy phase of the wave team (slots 22 -> 23 -> 28 -> 4): prologue + ahist zero, the policy loop, the mean
-    sel = (R[:, 16] <= 64) & (R[:, [22, 23, 28, 4]] > 0).all(1)
-    q = np.diff(R[sel][:, [22, 23, 28, 4]], axis=1)
-    print("policy split (<= 64 agents, %d env-steps), medians: prologue %d, policy loop %d, mean action %d"
-          % ((int(sel.sum()),) + tuple(int(x) for x in np.median(q, 0))))
+    # the policy phase of the wave team (slots 22 -> 9 -> 10 -> 11 -> 23 -> 28 -> 4): to few_agents, its views and
+    # psync, agent_phase's entry, ahist zero + psync, the policy loop, the mean action
+    cols = [22, 9, 10, 11, 23, 28, 4]
+    sel = (R[:, 16] <= 64) & (R[:, cols] > 0).all(1)
+    q = np.diff(R[sel][:, cols], axis=1)
+    print("policy split (<= 64 agents, %d env-steps), medians: to few_agents %d, views+psync %d, agent_phase entry %d, "
+          "ahist zero %d, policy loop %d, mean action %d" % ((int(sel.sum()),) + tuple(int(x) for x in np.median(q, 0))))
 for lab, m in (("<= 64 agents", nag <= 64), ("65-128 agents", (nag > 64) & (nag <= 128)), ("> 128 agents", nag > 128)):
     if m.any():
         print("%s: %d env-steps, median %d cycles per step; phase medians %s" % (
