@@ -19,9 +19,11 @@
 namespace mfx {
 
 // Diagnostic build only (-DMFX_STAMPS, build/libmagent_stamps.so): per-phase s_memtime deltas of
-// k_rollout go to a stamp buffer nobody else reads.  The real build compiles these to nothing.
+// k_rollout go to a stamp buffer nobody else reads.  The real build compiles these to nothing.  The buffer pointer
+// sits in constant memory: a scalar load, so a stamp does not wait (vmcnt) for the stores the phase before it left in
+// flight, as a vector load of a __device__ pointer did (which read those stores' latency into the phase).
 #ifdef MFX_STAMPS
-__device__ unsigned long long* g_stamps;
+__constant__ unsigned long long* g_stamps;
 constexpr int kStampW = 32;                  // stamps per env row
 #define MFX_STAMP(i)                                                                        \
     do {                                                                                    \
