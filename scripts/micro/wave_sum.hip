@@ -34,6 +34,25 @@ __global__ void k_check(const float* in, float* out, int n) {
     out[(w * 64 + t) * 2] = wave_sum_fast(x);
     out[(w * 64 + t) * 2 + 1] = wave_sum_ref(x);
 }
+// the DPP inclusive scan of step_big.inc (wave_incl_scan) against a serial prefix
+template <int kCtrl, int kRows = 0xF>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, kRows, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += dpp_u32<0x111>(x);
+    x += dpp_u32<0x112>(x);
+    x += dpp_u32<0x114>(x);
+    x += dpp_u32<0x118>(x);
+    x += dpp_u32<0x142, 0xA>(x);
+    x += dpp_u32<0x143, 0xC>(x);
+    return x;
+}
+__global__ void k_scan(const uint32_t* in, uint32_t* out, int n) {
+    const int t = threadIdx.x & 63, w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= n) return;
+    out[w * 64 + t] = wave_incl_scan(in[w * 64 + t]);
+}
 template <bool kFast>
 __global__ void k_chain(float* io, int iters) {
     float x = io[threadIdx.x];
@@ -58,6 +77,23 @@ int main() {
     for (size_t i = 0; i < h.size(); ++i)
         if (std::memcmp(&o[2 * i], &o[2 * i + 1], 4) != 0) ++bad;
     printf("wave_sum permlane/DPP vs butterfly: %ld mismatching lanes of %zu\n", bad, h.size());
+    {
+        std::vector<uint32_t> hi(h.size()), ho(h.size());
+        for (auto& v : hi) v = g() & 0xFFFF;
+        uint32_t *d_i, *d_o;
+        hipMalloc(&d_i, hi.size() * 4);
+        hipMalloc(&d_o, hi.size() * 4);
+        hipMemcpy(d_i, hi.data(), hi.size() * 4, hipMemcpyHostToDevice);
+        k_scan<<<n / 4, 256>>>(d_i, d_o, n);
+        hipMemcpy(ho.data(), d_o, ho.size() * 4, hipMemcpyDeviceToHost);
+        long sbad = 0;
+        for (int w = 0; w < n; ++w) {
+            uint32_t acc = 0;
+            for (int l = 0; l < 64; ++l) { acc += hi[w * 64 + l]; if (ho[w * 64 + l] != acc) ++sbad; }
+        }
+        printf("wave_incl_scan DPP vs serial prefix: %ld mismatching lanes of %zu\n", sbad, hi.size());
+        bad += sbad;
+    }
     float* d_io;
     hipMalloc(&d_io, 256);
     hipMemcpy(d_io, h.data(), 256, hipMemcpyHostToDevice);
