@@ -547,34 +547,46 @@ __global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __
 
 // ------------------------------------------------------------------------------------------ rollout rows
 // The compact row list of one group of a rollout batch: rows e * rowcap + j for j < n_e (n_e = the group's
-// size in the [E][G] counts), in env order.  One workgroup: a scan over E counts.
-__global__ void __launch_bounds__(1024) k_qnet_rows(const int32_t* __restrict__ counts, int E, int G, int g, int rowcap,
-                                                    int32_t* __restrict__ rows, int32_t* __restrict__ total) {
-    __shared__ int part[1024];
-    const int t = threadIdx.x, per = (E + 1023) / 1024;
-    const int e0 = min(E, t * per), e1 = min(E, e0 + per);
+// size in the [E][G] counts, capped at rowcap), in env order.  Workgroup b takes envs [64 b, 64 b + 64): it sums the
+// counts before its chunk itself (at most E loads, from L2), scans its 64 counts in one wave and writes its rows with
+// consecutive lanes on consecutive rows; the last chunk's workgroup writes the total.  (Was one workgroup for the
+// whole batch, each lane writing its envs' rows one by one: 0.29 ms per call at 8192 envs, 2.5 % of the MFAC loop.)
+constexpr int kRowsEnvs = 64;
+__global__ void __launch_bounds__(256) k_qnet_rows(const int32_t* __restrict__ counts, int E, int G, int g, int rowcap,
+                                                   int32_t* __restrict__ rows, int32_t* __restrict__ total) {
+    __shared__ int red[4];
+    __shared__ int cnt[kRowsEnvs], off[kRowsEnvs];
+    __shared__ int chunk_total;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int e0 = blockIdx.x * kRowsEnvs, e1 = min(E, e0 + kRowsEnvs);
     int s = 0;
-    for (int e = e0; e < e1; ++e) s += min(counts[e * G + g], rowcap);
-    part[t] = s;
+    for (int e = t; e < e0; e += blockDim.x) s += min(counts[e * G + g], rowcap);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) red[wid] = s;
+    if (t < kRowsEnvs) {
+        const int c = e0 + t < e1 ? min(counts[(e0 + t) * G + g], rowcap) : 0;
+        int inc = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        cnt[t] = c;
+        off[t] = inc - c;
+        if (t == kRowsEnvs - 1) chunk_total = inc;
+    }
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {                 // inclusive scan (Hillis-Steele)
-        const int v = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    const int base = red[0] + red[1] + red[2] + red[3];
+    for (int k = 0; k < e1 - e0; ++k) {
+        const int m = cnt[k], o = base + off[k], e = e0 + k;
+        for (int j = t; j < m; j += blockDim.x) rows[o + j] = e * rowcap + j;
     }
-    int off = part[t] - s;
-    for (int e = e0; e < e1; ++e) {
-        const int m = min(counts[e * G + g], rowcap);
-        for (int j = 0; j < m; ++j) rows[off + j] = e * rowcap + j;
-        off += m;
-    }
-    if (t == 1023) *total = part[1023];
+    if (e1 == E && t == 0) *total = base + chunk_total;
 }
 
 hipError_t launch_rollout_rows(const int32_t* counts, int E, int G, int g, int rowcap, int32_t* rows, int32_t* total,
                                hipStream_t st) {
-    k_qnet_rows<<<1, 1024, 0, st>>>(counts, E, G, g, rowcap, rows, total);
+    const int grid = E > 0 ? (E + kRowsEnvs - 1) / kRowsEnvs : 1;   // (E = 0: one workgroup writes the total 0)
+    k_qnet_rows<<<grid, 256, 0, st>>>(counts, E, G, g, rowcap, rows, total);
     return hipGetLastError();
 }
 
