@@ -29,6 +29,7 @@ episode statistics, running return) bit for bit; it also reads the device and qu
 (rollout_check).  The line's "check" records it; a mismatch exits non-zero.
 """
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -44,6 +45,38 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 MAP, N_SIDE = 64, 128
 BYTES_PER_AGENT_STEP = 4 * (1183 + 34) + 4 + 4 + 1 + 4 + 64      # 4,945 B
 HBM_PEAK_GBS = 8000.0                                           # MI355X spec (MI355X_MICROARCH.md)
+LIB = os.path.join(PKG, "build", "libmagent.so")
+
+
+def lib_sha16(path=LIB):
+    """Content hash of the engine library: the key under which PMC counters of a build are filed (a counter file
+    of another build is never attached to this build's line)."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def measure_ceiling(eng, total_bytes, reps=2):
+    """The HBM write ceiling of this GPU, measured in this process after the clock (report a
+    measured stream peak beside the nominal one): a write-only float4 stream of the same byte count as one timed
+    launch's algorithmic bytes over the same view buffer, in each store shape of BattleBatch.STORE_SHAPES, best
+    of `reps` per shape.  None when the buffer is too small to leave the caches (few envs)."""
+    import ctypes
+    ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
+    eng._check(eng._dll.mfx_battle_rollout_buffer(eng.game, b"view", 0, ctypes.byref(ptr), ctypes.byref(n)),
+               "rollout_buffer")
+    if n.value < (1 << 30):
+        return None
+    total = max(int(total_bytes), n.value, 16 << 30)
+    best = [0.0] * len(eng.STORE_SHAPES)
+    for _ in range(reps):
+        for sh in range(len(best)):
+            best[sh] = max(best[sh], eng.store_ceiling(total, sh))
+    k = max(range(len(best)), key=lambda i: best[i])
+    return {"peak": best[k], "shape": eng.STORE_SHAPES[k], "bytes": total, "region_bytes": n.value,
+            "per_shape_gbs": dict(zip(eng.STORE_SHAPES, best)),
+            "what": "write-only float4 stream (mfx_store_ceiling, csrc/diag_kernels.hip) of the timed launch's "
+                    "algorithmic bytes over the same view buffer, same process and GPU, after the clock; best of "
+                    "%d per shape" % reps}
 
 
 def parse(argv=None):
@@ -83,11 +116,21 @@ def parse(argv=None):
                     help="rush: the on-device synthetic policy (the metric); qnet: two random-init mean-field Q "
                          "networks (ValueNet, algo/base.py:123-183) on the HIP forward, one per group; mfac: two "
                          "random-init MFAC actor-critic networks (algo/ac.py:219-276) on the HIP forward + draw")
+    ap.add_argument("--no-ceiling", dest="ceiling", action="store_false",
+                    help="skip the measured write ceiling after the clock (roofline.measured_peak)")
+    ap.add_argument("--split", type=int, default=None,
+                    help="learned-policy modes: the envs as this many engines on their own HIP streams (overlap; "
+                         "default 2 for mfac -- 1.016e8 -> 1.051e8 agent-steps/s on one box, profiles/r06_mfac.txt -- "
+                         "1 for qnet)")
+    ap.add_argument("--dense-view", action="store_true",
+                    help="mfac: the view layer over all 1,183 inputs (A/B; default: the engine's view support)")
     ap.add_argument("--check-envs", type=int, default=8,
                     help="envs per rank replayed on the C oracle after the timed region (0: no check)")
     a = ap.parse_args(argv)
     if a.envs is None and a.total_envs is None and a.policy != "rush":
         a.envs = 8192                 # the network forward bounds these modes (1.2 / 3.4 MFLOP per agent-step)
+    if a.split is None:
+        a.split = 2 if a.policy == "mfac" else 1
     if a.envs is None and a.total_envs is None:
         # 64x64: 131072 envs per GPU (~160 GB of observation buffers, 56 % of the HBM) -- a launch has a fixed
         # cost (ramp-up and the tail of the persistent grid: the last env of each of 1280 workgroups), amortised
@@ -145,9 +188,9 @@ def _free_port():
     return p
 
 
-def launch_ranks(n, argv):
-    """Start n rank processes of this script (torch.distributed.run's env contract, 127.0.0.1
-    rendezvous) and wait for them.  Called before anything in this process touches the GPU; the
+def launch_ranks(n, argv, script=None):
+    """Start n rank processes of this script -- or of `script` (scripts/bench_ising.py shares the launcher) --
+    (torch.distributed.run's env contract, 127.0.0.1 rendezvous) and wait for them.  Called before anything in this process touches the GPU; the
     ranks are fresh children, so no GPU context is ever inherited or exec'd over.  If one rank
     fails the others are stopped (they would wait at a barrier).  Returns the worst exit status."""
     port = _free_port()
@@ -155,7 +198,7 @@ def launch_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(script or __file__)] + list(argv), env=env))
     status = 0
     live = list(procs)
     while live:
@@ -352,8 +395,15 @@ def main_qnet(args):
     of each group's model on the observation in the rollout buffers (mfx_qnet_act_rollout: greedy Q;
     mfx_acnet_act_rollout: the MFAC policy and its draw), then one k_rollout launch that acts with those actions,
     steps and observes (mfx_battle_rollout_policy_step).  Random-init networks (torch modules, packed once); the
-    value counts agent-steps as the rush line does.  The roofline is the forward's: f32 MFMA FLOPs over the two
-    forwards' HIP-event time."""
+    value counts agent-steps as the rush line does.  The roofline is the forward's: f32 MFMA FLOPs (the MFMAs the
+    kernels execute) over the two forwards' HIP-event time.
+
+    --split H: the envs as H engines of E / H envs, each stepping on its own HIP stream with the same networks, so
+    one engine's env step (k_rollout: HBM-bound observation writes) runs while another's forward (MFMA) does --
+    the loop of senario_battle.play (:96-171) on H independent env batches.  mfac: the view layer runs over the
+    inputs the engine's observation can make non-zero (BattleBatch.view_support, bit-identical, --dense-view: off).
+    After the clock the same steps run once more with every engine on one stream and HIP events around each
+    phase: the line's kernel_ms (forward) and env_step_ms (k_rollout) per step, serialised."""
     import torch
     import battle_driver as bd
     from mfrl_amd.algo.nets import ACNet, QNet
@@ -361,11 +411,19 @@ def main_qnet(args):
     from mfrl_amd.policy import ACNetHIP, QNetHIP
     torch.cuda.set_device(0)
     E = args.envs if args.total_envs is None else args.total_envs
-    stream = torch.cuda.current_stream()
+    H = max(1, min(args.split, E))
+    if H > 1 and args.policy != "mfac":
+        raise SystemExit("bench.py: --split needs --policy mfac (the QNet forward keeps per-network scratch)")
+    sizes = [E // H + (1 if h < E % H else 0) for h in range(H)]
+    main = torch.cuda.current_stream()
+    streams = [main] + [torch.cuda.Stream() for _ in range(H - 1)]
     left, right = bd.block_positions(args.map, args.agents // 2)
     os.environ.setdefault("MFX_SMALL_E", "0")                # (the fused k_rollout path at any E)
-    eng = BattleBatch(args.map, E, stream=stream)
-    eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.0, seed=1234)
+    engs = []
+    for h in range(H):
+        eng = BattleBatch(args.map, sizes[h], stream=streams[h])
+        eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.0, seed=1234 + 7919 * h)
+        engs.append(eng)
     torch.manual_seed(7)
     pols = []
     ac = args.policy == "mfac"
@@ -374,43 +432,75 @@ def main_qnet(args):
             pols.append(ACNetHIP((13, 13, 7), (34,), 21, True).load(ACNet((13, 13, 7), (34,), 21, use_mf=True).cuda()))
         else:
             pols.append(QNetHIP((13, 13, 7), (34,), 21, True).load(QNet((13, 13, 7), (34,), 21, True).cuda()))
-    flop_per_agent = ACNET_FLOP_PER_AGENT if ac else QNET_FLOP_PER_AGENT
+    torch.cuda.synchronize()
+    support = ac and not args.dense_view
     step_no = [0]
-    steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
+    steps_buf = [torch.zeros(n, dtype=torch.int64, device="cuda") for n in sizes]
 
     def agent_steps():
-        eng.rollout_copy("agent_steps", steps_buf)
-        return steps_buf.sum()
+        tot = torch.zeros((), dtype=torch.int64, device="cuda")
+        for h, eng in enumerate(engs):
+            eng.rollout_copy("agent_steps", steps_buf[h])
+            eng.sync()
+            tot += steps_buf[h].sum()
+        return tot
 
-    def one_step(evs=None):
-        if evs:
-            evs[0].record(stream)
+    def act(h):
         for g in range(2):
             if ac:
-                pols[g].act_rollout(eng, g, 1234, step_no[0])
+                pols[g].act_rollout(engs[h], g, 1234 + 7919 * h, step_no[0], support=support)
             else:
-                pols[g].act_rollout(eng, g)
-        step_no[0] += 1
-        if evs:
-            evs[1].record(stream)
-        eng.rollout_policy_step()
+                pols[g].act_rollout(engs[h], g)
 
-    eng.rollout_policy_observe()
+    def one_step():
+        for h, eng in enumerate(engs):
+            with torch.cuda.stream(streams[h]):
+                act(h)
+                eng.rollout_policy_step()
+        step_no[0] += 1
+
+    for h, eng in enumerate(engs):
+        with torch.cuda.stream(streams[h]):
+            eng.rollout_policy_observe()
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     a0 = agent_steps()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(evs[k])
+        one_step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     units = float((agent_steps() - a0).item())
-    fwd_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    eng.rollout_check()
-    flops = flop_per_agent * units / args.steps
+    # the phases, serialised: every engine on the main stream, events around each engine's forwards and step
+    n_ph = max(1, min(args.steps, 6))
+    evs = []
+    for h, eng in enumerate(engs):
+        eng.set_stream(main)
+    for k in range(n_ph):
+        for h, eng in enumerate(engs):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(main)
+            act(h)
+            e[1].record(main)
+            eng.rollout_policy_step()
+            e[2].record(main)
+            evs.append(e)
+        step_no[0] += 1
+    torch.cuda.synchronize()
+    fwd_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / n_ph
+    env_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / n_ph
+    for eng in engs:
+        eng.rollout_check()
+    units_step = units / args.steps
+    if ac:
+        kv = pols[0].input_support_size() or 1183
+        flop_dense = ACNET_FLOP_PER_AGENT
+        flop_per_agent = 2 * (kv * 256 + 34 * 256 + 512 * 512 + 512 * 21)
+    else:
+        flop_dense = flop_per_agent = QNET_FLOP_PER_AGENT
+    flops = flop_per_agent * units_step
     what = ("learned MFAC policy (HIP actor-critic forward + draw)" if ac else
             "learned MF-Q policy (HIP QNet forward)")
     line = {"metric": "agent-steps/sec (env.step+obs) Battle %dx%dx%d agents, %s" % (args.map, args.map, args.agents,
@@ -418,14 +508,23 @@ def main_qnet(args):
             "value": units / (t1 - t0), "unit": "agent-steps/s", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * (t1 - t0) / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (random-init networks)",
-            "config": {"workload": "Battle %dx%d, %d envs, two %s (one per group), forward + fused step per step"
-                                   % (args.map, args.map, E, "MFAC networks" if ac else "mean-field QNets"),
-                       "envs_per_gpu": E, "policy": args.policy},
+            "config": {"workload": "Battle %dx%d, %d envs, two %s (one per group), forward + fused step per step%s"
+                                   % (args.map, args.map, E, "MFAC networks" if ac else "mean-field QNets",
+                                      "; the envs as %d engines on %d HIP streams" % (H, H) if H > 1 else ""),
+                       "envs_per_gpu": E, "policy": args.policy, "engines": H,
+                       "view_inputs": (pols[0].input_support_size() or 1183) if ac else 1183},
             "roofline": {"bound": "mfma", "achieved": flops / (fwd_ms * 1e-3) / 1e12, "peak": F32_MFMA_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": flops / (fwd_ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS,
                          "traffic": None, "kernel": "k_acnet (x2 groups)" if ac else "k_qnet_conv + k_qnet_head (x2 groups)",
-                         "kernel_ms": fwd_ms, "flop_per_unit": flop_per_agent,
-                         "units_per_step": units / args.steps}}
+                         "kernel_ms": fwd_ms, "env_step_ms": env_ms,
+                         "kernel_ms_is": "the forwards (both groups, every engine) of one step, serialised after the "
+                                         "clock on one stream (HIP events; mean of %d steps); env_step_ms: the k_rollout "
+                                         "step + observation of every engine the same way" % n_ph,
+                         "flop_per_unit": flop_per_agent, "flop_per_unit_dense": flop_dense,
+                         "flop_is": "the MFMA FLOPs executed per agent (the view layer over the inputs the "
+                                    "observation can make non-zero when view_inputs < 1183); flop_per_unit_dense: the "
+                                    "dense network's",
+                         "units_per_step": units_step}}
     print(json.dumps(line), flush=True)
     return 0
 
@@ -531,6 +630,8 @@ def main():
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
     check = run_check(eng, args, E, [left, right], env_seed(1234, rank), world)
+    # the measured write ceiling of this GPU (after the check: it overwrites the view buffer)
+    ceiling = measure_ceiling(eng, BYTES_PER_AGENT_STEP * local_units / len(chunks)) if args.ceiling else None
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         steps_per_timed_launch = args.steps / len(chunks)       # the mean launch kernel_ms is
@@ -542,7 +643,9 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("envs") == E and pm.get("map", MAP) == args.map and pm.get("substeps", 1) == S:
+            # counters are attached only when they were collected on this build of the library at this shape
+            if (pm.get("envs") == E and pm.get("map", MAP) == args.map and pm.get("substeps", 1) == S
+                    and pm.get("lib_sha16") == lib_sha16()):
                 traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_step"))
         strong = args.total_envs is not None
         kern = {"k_rollout_obs+k_rollout": "k_rollout"}.get(path, path)
@@ -579,6 +682,14 @@ def main():
                                          "collectives), / their count; %g step(s) per launch"
                                          % (len(chunks), len(segs), steps_per_timed_launch),
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch,
+                         "measured_peak": ceiling["peak"] if ceiling else None,
+                         "frac_measured": achieved / ceiling["peak"] if ceiling else None,
+                         "measured_peak_detail": ceiling,
+                         "traffic_is": ("HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950) and WRITE_SIZE "
+                                        "passes of this library build (lib_sha16 %s), %s" % (lib_sha16(), pmc))
+                                       if traffic is not None else
+                                       "null: no counter file of this library build (lib_sha16 %s) at this shape"
+                                       % lib_sha16(),
                          "grid": grid, "lds_bytes": lds},
             "cpu_baseline": None,
             "episodes": {"finished": red[0], "return_mean": [red[1] / max(red[0], 1.0), red[2] / max(red[0], 1.0)],

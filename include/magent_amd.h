@@ -148,6 +148,10 @@ int mfx_battle_rollout_sum_lanes(void *game, int n_agents, int *lanes);
  * set_action / step / reward / mean action / clear_dead / restart and writes the next observation.  The
  * mean-action buffer then holds each group's former_act_prob (zeros at an episode's first step). */
 int mfx_battle_rollout_policy_step(void *game, int mode);
+/* The inputs of group `group`'s observation view that can be non-zero (Map.cc:130-218): mask[n] (n = view_h *
+ * view_w * n_ch, NHWC) = 1 for every channel of a cell inside the view range and for the minimap channels of the
+ * cells outside it, else 0 (never written: always zero). */
+int mfx_battle_view_support(void *game, int group, uint8_t *mask, int n);
 /* Diagnostic build only (libmagent_stamps.so): per-phase s_memtime stamps [E][16]. */
 int mfx_battle_set_stamp_buffer(void *d_buf);
 
@@ -195,11 +199,18 @@ int mfx_qnet_set_weights(void *handle, const float *d_blob, size_t n_floats, voi
 /* n agents: view [n][1183], feature [n][F], prob [n][A] (mean field, else null) -> q [n][A], act [n] */
 int mfx_qnet_forward(void *handle, const float *d_view, const float *d_feat, const float *d_prob, int n, float *d_q,
                      int32_t *d_act, void *stream);
-/* group g of a rollout batch -> the rollout's action buffer (live rows); d_rows: E * rowcap + 1 ints scratch */
+/* group g of a rollout batch -> the rollout's action buffer (live rows); d_rows: E * rowcap ints scratch, d_total:
+ * 1 + ceil(E / 64) ints (the row count, then per-64-env chunk totals) -- one buffer of E * rowcap + 1 + ceil(E / 64)
+ * ints with d_total = d_rows + E * rowcap is the usual layout */
 int mfx_qnet_act_rollout(void *handle, const float *d_view, const float *d_feat, const int32_t *d_counts,
                          const double *d_mean, int mean_stride, int E, int G, int g, int rowcap, int32_t *d_rows,
                          int32_t *d_total, int32_t *d_act, void *stream);
 /* (the row count stays on the device: the kernels are launched for E * rowcap rows and read *d_total) */
+
+/* The compact row list the act_rollout calls build: d_rows[i] = e * rowcap + j over envs e, j < min(counts[e][g],
+ * rowcap), in env order; d_total[0] = the row count (d_total: 1 + ceil(E / 64) ints). */
+int mfx_rollout_rows(const int32_t *d_counts, int E, int G, int g, int rowcap, int32_t *d_rows, int32_t *d_total,
+                     void *stream);
 
 /* The actor-critic network of ActorCritic._create_network (algo/ac.py:48-98) / MFAC._create_network (:219-276)
  * and its act, tf.multinomial(log(policy)) (:43-46, :213-217), forward only, f32 MFMA
@@ -213,12 +224,17 @@ int mfx_acnet_blob_size(int view_floats, int feature, int n_action, int use_mf, 
 int mfx_acnet_create(int view_floats, int feature, int n_action, int use_mf, void **handle);
 int mfx_acnet_destroy(void *handle);
 int mfx_acnet_set_weights(void *handle, const float *d_blob, size_t n_floats, void *stream);
+/* The view inputs that can be non-zero, mask[n] (n = view_floats; e.g. mfx_battle_view_support), or null for the dense
+ * order: later forwards run the view layer over the supported inputs only, bit-identical when the others are zero
+ * (the caller's contract).  input_support_size: the inputs the view layer runs over (0 = dense). */
+int mfx_acnet_set_input_support(void *handle, const uint8_t *mask, int n, void *stream);
+int mfx_acnet_input_support_size(void *handle, int *k);
 /* n agents: view [n][view_floats], feature [n][F], prob [n][A] float32 (the MF value head; else null) ->
  * policy [n][A], value [n], act [n] (each may be null); row i drawn with (seed, step, group 0, row i) */
 int mfx_acnet_forward(void *handle, const float *d_view, const float *d_feat, const float *d_prob, int n,
                       float *d_policy, float *d_value, int32_t *d_act, uint32_t seed, uint32_t step, void *stream);
 /* group g of a rollout batch -> sampled actions in the rollout's action buffer (live rows; row j of env e drawn
- * with (seed, step, g, e * rowcap + j)); d_rows: E * rowcap + 1 ints scratch; nothing is read back */
+ * with (seed, step, g, e * rowcap + j)); d_rows / d_total as mfx_qnet_act_rollout's; nothing is read back */
 int mfx_acnet_act_rollout(void *handle, const float *d_view, const float *d_feat, const int32_t *d_counts, int E,
                           int G, int g, int rowcap, int32_t *d_rows, int32_t *d_total, int32_t *d_act, uint32_t seed,
                           uint32_t step, void *stream);
@@ -233,6 +249,13 @@ int mfx_acnet_act_rollout(void *handle, const float *d_view, const float *d_feat
 int mfx_rows_copy(int n_cols, void *const *dst, const void *const *src, const int64_t *row_bytes, const int64_t *d_idx,
                   int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap, int64_t n, void *stream);
 int mfx_rows_copy_error(int64_t *bad_index, void *stream);
+
+/* ---------------------------------------------------------------- measurement */
+/* The HBM write ceiling on this device, measured in-process beside the bench (csrc/diag_kernels.hip): total_bytes
+ * of float4 stores over the device region [d_buf, d_buf + region_bytes), wrapping; shape 0..7: bit 0 = nontemporal
+ * stores, bits 1-2 = 4 / 8 / 16 KiB chunks, one workgroup per chunk, or (3) 4 KiB chunks on a persistent grid;
+ * *ms = HIP-event time (synchronises). */
+int mfx_store_ceiling(void *d_buf, size_t region_bytes, size_t total_bytes, int shape, void *stream, float *ms);
 
 /* ---------------------------------------------------------------- library */
 const char *mfx_last_error(void);

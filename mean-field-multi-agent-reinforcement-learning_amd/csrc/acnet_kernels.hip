@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "mfx_common.h"
 #include "policy_gemm.h"
@@ -58,6 +59,16 @@ struct ACNetDev {
     const float* w[kABlocks];
     const float* img[kAImg];
     int V, Vp, F, Fp, A, Ap, use_mf;
+    // The view's input support (mfx_acnet_set_input_support; null: the dense order).  The view layer then runs over
+    // the vK inputs that can be non-zero only -- e.g. the Battle view's cells outside the view circle carry nothing
+    // but the two minimap channels (Map.cc:130-218), 280 of 1,183 inputs always zero -- in a packed order: packed
+    // input 16 ch + j is view float vdesc[8 ch + 4] + byte j of vdesc[8 ch .. 8 ch + 3], and vimg is the image of
+    // wv's rows in that order (mfx_acnet_set_input_support keeps the dense chain's order of the supported inputs).  A
+    // skipped input is an exact zero, so each fma it leaves out of a chain would only have added 0 * w: the same
+    // result bit for bit (the MFMA accumulates as an fmaf chain, MI355X_MICROARCH.md).
+    const uint32_t* vdesc;
+    const float* vimg;
+    int vK;
 };
 
 // x / 0.1f, correctly rounded (the reference's dense / 0.1): q = x * 10, one fma residual and one fma correction --
@@ -98,7 +109,7 @@ constexpr size_t kAcnetImgLdsSmem = kImgSmem + (size_t)kHeF * kAH * 4 + 3 * 1024
 
 // kImg: the layers run wg_gemm_i over the weight images (direct-to-LDS staging; the default), else wg_gemm_t (A/B:
 // MFX_ACNET_IMG=0).  GEMM<MT, NCH, kZero>(block, image, K, v_at, acc) picks the form.
-template <typename PT, bool kMF, bool kHeLds, bool kImg>
+template <typename PT, bool kMF, bool kHeLds, bool kImg, bool kPack = false>
 __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const float* __restrict__ view, size_t view_ld,
                                                   const float* __restrict__ feat, size_t feat_ld,
                                                   const PT* __restrict__ prob, size_t prob_ld, QRowMap rm, int n,
@@ -149,6 +160,18 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
         // (columns past V read float V - 1: its weights are zero)
         float* vring = bsm + 2 * kImgBuf + kHeF * kAH;
         const float* vsrc[4];
+        // the packed order's chunk descriptors through the constant address space: scalar loads, each issued one
+        // chunk before its use (a vector load here would wait, vmcnt being in order, for the chunk's image loads)
+        // kPack: the packed order's chunk descriptors through the constant address space -- scalar loads, each issued
+        // one chunk before its use (volatile: not sunk to the use), waited for by the chunk-end barrier's lgkmcnt(0)
+        typedef const volatile __attribute__((address_space(4))) uint32_t* cdesc_t;
+        cdesc_t dq = (cdesc_t)p.vdesc;
+        asm volatile("" : "+s"(dq));
+        uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0;
+        auto dload = [&](int ch) {
+            d0 = dq[8 * ch]; d1 = dq[8 * ch + 1]; d2 = dq[8 * ch + 2]; d3 = dq[8 * ch + 3]; d4 = dq[8 * ch + 4];
+        };
+        if (kPack) dload(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int a = min(tile * kQHeadWaves * 16 + 4 * (4 * wid + q) + (lane >> 4), n - 1);
@@ -157,7 +180,14 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
         const int V = p.V;
         auto view_issue = [&](int ch) {
             float* dst = vring + (ch % 3) * 1024 + wid * 256;
-            const int k = min(16 * ch + c, V - 1);
+            int k;
+            if constexpr (kPack) {                                 // the packed order
+                const uint32_t lo = (c & 4) ? d1 : d0, hi = (c & 4) ? d3 : d2, w = (c & 8) ? hi : lo;
+                k = (int)(d4 + ((w >> (8 * (c & 3))) & 255u));
+                dload(ch + 1);
+            } else {
+                k = min(16 * ch + c, V - 1);
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 __builtin_amdgcn_global_load_lds((const void*)(vsrc[q] + k),
@@ -172,7 +202,8 @@ __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const
         };
         bias_init(hv, W[1], h);
         if (!(MFX_ACNET_SKIP & 1))
-            wg_gemm_i<16, 0, false, 4>(I[0], p.Vp, vat, bsm, hv, [&](int ch) { view_issue(ch + 2); });
+            wg_gemm_i<16, 0, false, 4>(kPack ? p.vimg : I[0], kPack ? p.vK : p.Vp, vat, bsm, hv,
+                                       [&](int ch) { view_issue(ch + 2); });
     } else {
         const float* vr = view + (size_t)row * view_ld + 4 * h;
         const int V = p.V;
@@ -354,7 +385,46 @@ struct ACNetHandle {
     float* img = nullptr;                 // the weight images (launch_weight_image), made by set_weights
     size_t img_n = 0;
     bool imaged = false;
+    // the view's input support (mfx_acnet_set_input_support): packed order, its chunk descriptors, wv's rows in that
+    // order (gathered, then imaged)
+    int vK = 0;                           // packed rows (a multiple of 16: pads are zero rows)
+    int vKn = 0;                          // supported inputs
+    int* vperm = nullptr;                 // [vK] view row of packed input p (-1: a zero pad row)
+    uint32_t* vdesc = nullptr;            // [(chunks + 2) * 8]
+    float* vrows = nullptr;               // [vK][256]
+    float* vimg = nullptr;
 };
+
+__global__ void k_gather_rows(const float* __restrict__ src, const int* __restrict__ idx, int rows, int cols,
+                              float* __restrict__ dst) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (size_t)rows * cols) {
+        const int r = idx[i / cols];
+        dst[i] = r >= 0 ? src[(size_t)r * cols + i % cols] : 0.f;
+    }
+}
+
+// wv's rows in the packed order -> the image the kernel reads (after set_weights and after a support change)
+int acnet_support_image(ACNetHandle* q, hipStream_t st) {
+    if (!q->vK || !q->imaged) return 0;
+    const size_t n = (size_t)q->vK * kAH;
+    k_gather_rows<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(q->dev.w[0], q->vperm, q->vK, kAH, q->vrows);
+    MFX_HIP(hipGetLastError());
+    MFX_HIP(launch_weight_image(q->vrows, q->vK, kAH, q->vimg, st));
+    q->dev.vdesc = q->vdesc;
+    q->dev.vimg = q->vimg;
+    q->dev.vK = q->vK;
+    return 0;
+}
+
+void acnet_support_free(ACNetHandle* q) {
+    for (void* x : {(void*)q->vperm, (void*)q->vdesc, (void*)q->vrows, (void*)q->vimg})
+        if (x) (void)hipFree(x);
+    q->vperm = nullptr; q->vdesc = nullptr; q->vrows = nullptr; q->vimg = nullptr;
+    q->vK = 0;
+    q->vKn = 0;
+    q->dev.vdesc = nullptr; q->dev.vimg = nullptr; q->dev.vK = 0;
+}
 
 // The imaged blocks: (blob block, row offset, K, N) of images 0..10 (ACNetDev::img).
 struct ImgDesc { int block, row0, K, N; };
@@ -426,6 +496,7 @@ MFX_API int mfx_acnet_destroy(void* handle) {
     if (!q) return 0;
     if (q->blob) (void)hipFree(q->blob);
     if (q->img) (void)hipFree(q->img);
+    acnet_support_free(q);
     delete q;
     return 0;
 }
@@ -444,6 +515,65 @@ MFX_API int mfx_acnet_set_weights(void* handle, const float* d_blob, size_t n_fl
                                     const_cast<float*>(q->dev.img[k]), (hipStream_t)stream));
     }
     q->imaged = true;
+    return acnet_support_image(q, (hipStream_t)stream);
+}
+
+// The view inputs that can be non-zero: mask[n] (n = view floats; 1 = may be non-zero), e.g. from
+// mfx_battle_view_support; null clears it (the dense order).  Every later forward / act_rollout skips the inputs
+// outside the support -- the caller's contract: they are exactly zero there (the engine's observation buffers are);
+// the results are then bit-identical to the dense order.
+MFX_API int mfx_acnet_set_input_support(void* handle, const uint8_t* mask, int n, void* stream) {
+    auto* q = static_cast<ACNetHandle*>(handle);
+    acnet_support_free(q);
+    if (!mask) return 0;
+    if (n != q->dev.V) return fail("acnet_set_input_support: %d entries, the view has %d floats", n, q->dev.V);
+    // The MFMA chain of one accumulator runs chunk by chunk, k-step s by k-step, lane group h by lane group (input
+    // 16 ch + 4 h + s; an fmaf chain, MI355X_MICROARCH.md).  The supported inputs keep that order: the i-th one in
+    // the dense chain takes the i-th place of the packed chain (chunk i / 16, k-step (i % 16) / 4, lane group i % 4,
+    // i.e. packed input 16 (i / 16) + 4 (i % 4) + (i % 16) / 4), so the packed chain is the dense one without its
+    // zero terms -- each fma(w, 0, acc) = acc -- and equal bit for bit.
+    std::vector<int> chain;
+    for (int ch = 0; 16 * ch < n; ++ch)
+        for (int st = 0; st < 4; ++st)
+            for (int hh = 0; hh < 4; ++hh) {
+                const int k = 16 * ch + 4 * hh + st;
+                if (k < n && mask[k]) chain.push_back(k);
+            }
+    if (chain.empty()) chain.push_back(0);                       // (an all-zero view: one zero-weight row)
+    const int K = (int)chain.size(), nch = (K + 15) / 16;
+    std::vector<int> orig((size_t)nch * 16, -1);                 // packed input -> view float (-1: a zero pad row)
+    for (int i = 0; i < K; ++i) orig[16 * (i / 16) + 4 * (i % 4) + (i % 16) / 4] = chain[i];
+    std::vector<uint32_t> desc((size_t)(nch + 2) * 8, 0u);
+    for (int ch = 0; ch < nch + 2; ++ch) {
+        int base = chain[K - 1];
+        for (int j = 0; j < 16 && ch < nch; ++j)
+            if (orig[16 * ch + j] >= 0) base = std::min(base, orig[16 * ch + j]);
+        desc[8 * ch + 4] = (uint32_t)base;
+        for (int j = 0; j < 16; ++j) {
+            const int o = ch < nch && orig[16 * ch + j] >= 0 ? orig[16 * ch + j] : base;   // (pad rows: zero weights)
+            if (o - base > 255) return fail("acnet_set_input_support: packed chunk %d spans %d floats", ch, o - base + 1);
+            desc[8 * ch + j / 4] |= (uint32_t)(o - base) << (8 * (j % 4));
+        }
+    }
+    std::vector<int> rows((size_t)nch * 16);                     // wv row of packed input p (pads: a zero row)
+    for (int p = 0; p < nch * 16; ++p) rows[p] = orig[p] >= 0 ? orig[p] : -1;
+    const int KR = nch * 16;                                     // packed rows, pads included
+    const size_t nimg = img_floats(KR, kAH / 16);
+    if (hipMalloc(&q->vperm, sizeof(int) * KR) != hipSuccess || hipMalloc(&q->vdesc, sizeof(uint32_t) * desc.size()) != hipSuccess ||
+        hipMalloc(&q->vrows, sizeof(float) * KR * kAH) != hipSuccess || hipMalloc(&q->vimg, sizeof(float) * nimg) != hipSuccess) {
+        acnet_support_free(q);
+        return fail("acnet_set_input_support: hipMalloc");
+    }
+    MFX_HIP(hipMemcpy(q->vperm, rows.data(), sizeof(int) * KR, hipMemcpyHostToDevice));
+    MFX_HIP(hipMemcpy(q->vdesc, desc.data(), sizeof(uint32_t) * desc.size(), hipMemcpyHostToDevice));
+    q->vK = KR;
+    q->vKn = K;
+    return acnet_support_image(q, (hipStream_t)stream);
+}
+
+// Inputs the view layer runs over (0: the dense order).
+MFX_API int mfx_acnet_input_support_size(void* handle, int* k) {
+    *k = static_cast<ACNetHandle*>(handle)->vKn;
     return 0;
 }
 
@@ -462,14 +592,16 @@ static int acnet_run(ACNetHandle* q, const float* view, size_t view_ld, const fl
         const char* pl = getenv("MFX_ACNET_PERSIST");               // A/B only: 0 = one workgroup per tile
         if (!(pl && atoi(pl) == 0)) grid = std::min(grid, (lds ? 2 : 1) * device_cus());
     }
-#define MFX_ACNET_LAUNCH1(PT, MF, LDS, IMG, PB)                                                                         \
-    k_acnet<PT, MF, LDS, IMG><<<grid, 256, IMG && LDS ? kAcnetImgLdsSmem : (LDS ? kAcnetLdsSmem : kQHeadSmem),         \
-                                st>>>(q->dev, view, view_ld, feat, feat_ld, PB, prob_ld, rm, n, d_n, policy, value, act,  \
-                                      seed, step, group)
+#define MFX_ACNET_LAUNCH1(PT, MF, LDS, IMG, PK, PB)                                                                     \
+    k_acnet<PT, MF, LDS, IMG, PK><<<grid, 256, IMG && LDS ? kAcnetImgLdsSmem : (LDS ? kAcnetLdsSmem : kQHeadSmem),     \
+                                    st>>>(q->dev, view, view_ld, feat, feat_ld, PB, prob_ld, rm, n, d_n, policy, value,   \
+                                          act, seed, step, group)
+    // (the packed view order: the image path with h_emb in LDS -- the view-ring form -- and a support set)
 #define MFX_ACNET_LAUNCH(PT, MF, LDS, PB)                                                                              \
     do {                                                                                                              \
-        if (img) MFX_ACNET_LAUNCH1(PT, MF, LDS, true, PB);                                                            \
-        else MFX_ACNET_LAUNCH1(PT, MF, LDS, false, PB);                                                               \
+        if (img && LDS && q->dev.vdesc) MFX_ACNET_LAUNCH1(PT, MF, LDS, true, LDS, PB);                               \
+        else if (img) MFX_ACNET_LAUNCH1(PT, MF, LDS, true, false, PB);                                                \
+        else MFX_ACNET_LAUNCH1(PT, MF, LDS, false, false, PB);                                                        \
     } while (0)
     const double* pd = static_cast<const double*>(prob);
     const float* pf = static_cast<const float*>(prob);

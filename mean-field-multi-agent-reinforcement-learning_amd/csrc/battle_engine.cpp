@@ -1315,8 +1315,10 @@ public:
                             // (the stepper's scratch for the items it takes back follows its LDS layout)
                             int pg = 0;
                             MFX_HIP_THROW(bigq_grid(gp, s.cap, s.acap, Rq, true, &pg, true));
-                            ro_q_grid = std::min(ro_q_grid, pg);
-                            ra.few_pipe = E <= ro_q_grid / 4;
+                            ra.few_pipe = E <= std::min(ro_q_grid, pg) / 4;
+                            // (the pipe grid only when the pipelined form stays: the queue-step form keeps its
+                            // full grid)
+                            if (ra.few_pipe) ro_q_grid = std::min(ro_q_grid, pg);
                         }
                         // env chunks (not pipelined): envs per launch by the state bytes one launch cycles through
                         ro_qchunks = 1;
@@ -2609,6 +2611,30 @@ MFX_API int mfx_battle_rollout_rowcap(void* game, int* rowcap) {
 }
 MFX_API int mfx_battle_rollout_mean_stride(void* game, int* stride) {
     *stride = MFX_ENV(game)->ra.mean_stride;
+    return 0;
+}
+// The inputs of group g's observation view that can be non-zero (Map::extract_view, Map.cc:130-218): every channel
+// of a cell inside the view range, only the minimap channels (group2channel(k) + 2, GridWorld.cc:396-409) of a cell
+// outside it.  mask[n], n = view_h * view_w * n_ch (the view's NHWC order): 1 = may be non-zero, 0 = always 0.
+MFX_API int mfx_battle_view_support(void* game, int group, uint8_t* mask, int n) {
+    BattleEngine* e = MFX_ENV(game);
+    if (group < 0 || group >= e->n_groups()) return mfx::fail("view_support: bad group");
+    if (!e->allocated) {                     // (once allocated, gp is the parameter set the device runs on)
+        try {
+            MFX_CHECK(e->build_params());
+        } catch (const std::exception& ex) {
+            return mfx::fail("%s", ex.what());
+        }
+    }
+    const mfx::TypeParams& T = e->gp.type[group];
+    const int NC = e->gp.n_ch, cells = T.view_w * T.view_h;
+    if (n != cells * NC) return mfx::fail("view_support: %d entries, the view has %d", n, cells * NC);
+    for (int c = 0; c < cells; c++)
+        for (int ch = 0; ch < NC; ch++) {
+            bool mm = false;
+            for (int k = 0; e->minimap && k < e->n_groups(); k++) mm = mm || ch == e->group2channel(k) + 2;
+            mask[c * NC + ch] = (uint8_t)(T.view_mask[c] || mm);
+        }
     return 0;
 }
 MFX_API int mfx_battle_group_capacity(void* game, int group, int* cap) {

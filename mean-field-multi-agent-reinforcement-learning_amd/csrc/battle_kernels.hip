@@ -30,8 +30,9 @@ constexpr int kStampW = 32;                  // stamps per env row
         __syncthreads();                                                                    \
         if (TID == 0 && g_stamps) {                                                         \
             g_stamps[stamp_row * kStampW + (i)] = __builtin_amdgcn_s_memtime();                  \
+            /* wall clock (100 MHz) at stamps 0 / 10 and the workgroup: scripts/timeline_rollout.py */ \
             if ((i) == 0) g_stamps[stamp_row * kStampW + 11] = __builtin_amdgcn_s_memrealtime();  \
-            if ((i) == 0) g_stamps[stamp_row * kStampW + 28] = blockIdx.x;                        \
+            if ((i) == 0) g_stamps[stamp_row * kStampW + 27] = blockIdx.x;                        \
             if ((i) == 10) g_stamps[stamp_row * kStampW + 12] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                                   \
     } while (0)

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -175,8 +176,13 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
     // draws (N - 1 accepted words plus rejections: ~0.5 N expected, bounded here by 2 N -- a walk past the end sets
     // the error word) + one chunk of read-ahead (k_ising_scan reads 64 words at a time; its prefetch clamps at the stride)
     const size_t per = (size_t)N + (size_t)episodes * ((size_t)N + (size_t)T * 4 * N) + 320;
-    const int blocks = (int)((per + 623) / 624);
-    const size_t W = (size_t)blocks * 624;
+    const size_t blocks_z = (per + 623) / 624;
+    const size_t W = blocks_z * 624;
+    // the per-step word offsets (k_ising_scan's off, k_ising_mfq's woff, the next episode's prev_off) are 32-bit
+    if (W > (size_t)UINT32_MAX)
+        return mfx::fail("ising mfq stream: %zu words per replica (episodes x T x 4 N) exceed the 32-bit word offsets; "
+                         "run fewer episodes per call or mode 'host'", W);
+    const int blocks = (int)blocks_z;
     // replicas per pass: a slot's word streams within 64 GB and a third of the free memory.  Big passes: the walk
     // is one latency-bound wave per replica, so a pass's walk takes about as long whatever its replicas -- 16384
     // replicas at 2000 steps: 3.41e10 spin-steps/s in 16-GB passes, 3.86e10 in 64-GB ones (MFX_ISING_PASS_GB: A/B only)

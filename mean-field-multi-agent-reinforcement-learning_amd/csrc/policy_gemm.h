@@ -260,7 +260,8 @@ struct QRowMap {
 };
 
 // The compact row list of one group of a rollout batch (policy_kernels.hip k_qnet_rows): rows e * rowcap + j for
-// j < min(n_e, rowcap) in env order, and their count in *total -- on the device, nothing read back.
+// j < min(n_e, rowcap) in env order, and their count in total[0] -- on the device, nothing read back.  total: 1 +
+// ceil(E / 64) ints (the chunks' totals follow the count).
 hipError_t launch_rollout_rows(const int32_t* counts, int E, int G, int g, int rowcap, int32_t* rows, int32_t* total,
                                hipStream_t st);
 

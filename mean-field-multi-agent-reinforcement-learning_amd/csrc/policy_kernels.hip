@@ -547,11 +547,21 @@ __global__ void __launch_bounds__(256, 2) k_qnet_head(QNetDev p, const float* __
 
 // ------------------------------------------------------------------------------------------ rollout rows
 // The compact row list of one group of a rollout batch: rows e * rowcap + j for j < n_e (n_e = the group's
-// size in the [E][G] counts, capped at rowcap), in env order.  Workgroup b takes envs [64 b, 64 b + 64): it sums the
-// counts before its chunk itself (at most E loads, from L2), scans its 64 counts in one wave and writes its rows with
-// consecutive lanes on consecutive rows; the last chunk's workgroup writes the total.  (Was one workgroup for the
-// whole batch, each lane writing its envs' rows one by one: 0.29 ms per call at 8192 envs, 2.5 % of the MFAC loop.)
+// size in the [E][G] counts, capped at rowcap), in env order.  Two launches over chunks of 64 envs: k_rows_chunk
+// scans each chunk's counts (one wave) into its total (total[1 + b]); k_qnet_rows gives workgroup b the sum of the
+// totals before its chunk (at most E / 64 loads) and writes the chunk's rows with consecutive lanes on consecutive
+// rows; the last chunk's workgroup writes the row count (total[0]).  (Round 5 summed the counts before the chunk in
+// every workgroup: O(E^2 / 64) loads, ~1 GB per call at 131072 envs -- ADVICE r5; round 4 ran one workgroup for the
+// whole batch: 0.29 ms per call at 8192 envs.)
 constexpr int kRowsEnvs = 64;
+__global__ void __launch_bounds__(64) k_rows_chunk(const int32_t* __restrict__ counts, int E, int G, int g, int rowcap,
+                                                   int32_t* __restrict__ total) {
+    const int e = blockIdx.x * kRowsEnvs + (int)threadIdx.x;
+    int c = e < E ? min(counts[e * G + g], rowcap) : 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (threadIdx.x == 0) total[1 + blockIdx.x] = c;
+}
+
 __global__ void __launch_bounds__(256) k_qnet_rows(const int32_t* __restrict__ counts, int E, int G, int g, int rowcap,
                                                    int32_t* __restrict__ rows, int32_t* __restrict__ total) {
     __shared__ int red[4];
@@ -560,7 +570,7 @@ __global__ void __launch_bounds__(256) k_qnet_rows(const int32_t* __restrict__ c
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int e0 = blockIdx.x * kRowsEnvs, e1 = min(E, e0 + kRowsEnvs);
     int s = 0;
-    for (int e = t; e < e0; e += blockDim.x) s += min(counts[e * G + g], rowcap);
+    for (int b = t; b < (int)blockIdx.x; b += blockDim.x) s += total[1 + b];
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     if (lane == 0) red[wid] = s;
     if (t < kRowsEnvs) {
@@ -580,12 +590,13 @@ __global__ void __launch_bounds__(256) k_qnet_rows(const int32_t* __restrict__ c
         const int m = cnt[k], o = base + off[k], e = e0 + k;
         for (int j = t; j < m; j += blockDim.x) rows[o + j] = e * rowcap + j;
     }
-    if (e1 == E && t == 0) *total = base + chunk_total;
+    if (e1 >= E && t == 0) *total = base + chunk_total;
 }
 
 hipError_t launch_rollout_rows(const int32_t* counts, int E, int G, int g, int rowcap, int32_t* rows, int32_t* total,
                                hipStream_t st) {
     const int grid = E > 0 ? (E + kRowsEnvs - 1) / kRowsEnvs : 1;   // (E = 0: one workgroup writes the total 0)
+    if (E > 0) k_rows_chunk<<<grid, kRowsEnvs, 0, st>>>(counts, E, G, g, rowcap, total);
     k_qnet_rows<<<grid, 256, 0, st>>>(counts, E, G, g, rowcap, rows, total);
     return hipGetLastError();
 }
@@ -722,6 +733,14 @@ static int qnet_run(QNetHandle* q, const float* view, size_t view_ld, const floa
 #undef MFX_QHEAD
         MFX_HIP(hipGetLastError());
     }
+    return 0;
+}
+
+// The compact row list act_rollout builds (k_rows_chunk + k_qnet_rows), on its own: rows of group g of [E][G] counts.
+MFX_API int mfx_rollout_rows(const int32_t* d_counts, int E, int G, int g, int rowcap, int32_t* d_rows, int32_t* d_total,
+                             void* stream) {
+    if (E < 0 || G < 1 || g < 0 || g >= G || rowcap < 1) return fail("rollout_rows: bad shape");
+    MFX_HIP(launch_rollout_rows(d_counts, E, G, g, rowcap, d_rows, d_total, (hipStream_t)stream));
     return 0;
 }
 

@@ -174,6 +174,34 @@ class BattleBatch:
         self._check(self._dll.mfx_battle_rollout_mean_stride(self.game, ctypes.byref(p)), "rollout_mean_stride")
         return p.value
 
+    STORE_SHAPES = tuple("%s per workgroup, %s%s" % (c, g, nt) for c, g in (
+        ("4 KiB", "one workgroup per chunk"), ("8 KiB", "one workgroup per chunk"), ("16 KiB", "one workgroup per chunk"),
+        ("4 KiB", "persistent grid (8 per CU)")) for nt in ("", ", nt"))       # mfx_store_ceiling shapes 0..7
+
+    def store_ceiling(self, total_bytes, shape, group=0):
+        """GB/s of a write-only float4 stream of total_bytes over this batch's view buffer of `group` (wrapping;
+        mfx_store_ceiling, shape index into STORE_SHAPES) on the engine's stream.  Overwrites the views: call it
+        only after their last use."""
+        ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self._dll.mfx_battle_rollout_buffer(self.game, b"view", group, ctypes.byref(ptr), ctypes.byref(n)),
+                    "rollout_buffer")
+        ms = ctypes.c_float()
+        self._dll.mfx_store_ceiling.restype = ctypes.c_int
+        self._check(self._dll.mfx_store_ceiling(ptr, n, ctypes.c_size_t(int(total_bytes)), int(shape),
+                                                ctypes.c_void_p(self.stream_handle()), ctypes.byref(ms)),
+                    "store_ceiling")
+        return (int(total_bytes) // 4096 * 4096) / (ms.value * 1e-3) / 1e9
+
+    def view_support(self, group):
+        """uint8 [view_h * view_w * n_ch] (the view's NHWC order): 1 where group `group`'s observation view can be
+        non-zero, 0 where it is always zero (cells outside the view range carry only the minimap channels)."""
+        n = int(np.prod(self.env.get_view_space(self.handles[group])))
+        mask = np.zeros(n, dtype=np.uint8)
+        self._dll.mfx_battle_view_support.restype = ctypes.c_int
+        self._check(self._dll.mfx_battle_view_support(self.game, int(group), mask.ctypes.data_as(ctypes.c_void_p), n),
+                    "view_support")
+        return mask
+
     def rollout_copy(self, name, dst, group=0, nbytes=None):
         """Copy a device rollout buffer into dst (numpy array or torch tensor, host or device)."""
         ptr = dst.data_ptr() if hasattr(dst, "data_ptr") else dst.ctypes.data

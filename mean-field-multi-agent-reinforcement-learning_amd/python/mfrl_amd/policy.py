@@ -14,6 +14,8 @@ from the torch module's by summation order only (|dq| ~1e-6 at these sizes, test
 """
 import ctypes
 
+import numpy as np
+
 import torch
 
 from . import check, lib
@@ -23,6 +25,12 @@ _P = ctypes.c_void_p
 
 def _ptr(t):
     return _P(t.data_ptr()) if t is not None else _P()
+
+
+def rows_scratch(E, rowcap):
+    """Ints of the act_rollout row-list scratch: E * rowcap rows, the row count, one total per 64-env chunk
+    (include/magent_amd.h, mfx_qnet_act_rollout)."""
+    return E * rowcap + 1 + (E + 63) // 64
 
 
 def _stream():
@@ -138,8 +146,8 @@ class QNetHIP:
         """Actions of group `group` of a BattleBatch rollout from its current observation buffers and
         former mean actions, written into the rollout's action buffer [E][G][rowcap] (live rows only)."""
         E, rc, G = eng.n_envs, eng.rowcap, len(eng.handles)
-        if self._rows is None or self._rows.numel() < E * rc + 1:
-            self._rows = torch.empty(E * rc + 1, dtype=torch.int32, device="cuda")
+        if self._rows is None or self._rows.numel() < rows_scratch(E, rc):
+            self._rows = torch.empty(rows_scratch(E, rc), dtype=torch.int32, device="cuda")
         ptr = {}
         for name in ("view", "feature", "group_num", "mean_action", "actions"):
             p, nb = _P(), ctypes.c_size_t()
@@ -224,14 +232,15 @@ class ACNetHIP:
         self.V, self.F, self.A, self.use_mf = V, int(feature_space[0]), int(num_actions), bool(use_mf)
         L = lib()
         for fn in ("mfx_acnet_create", "mfx_acnet_destroy", "mfx_acnet_set_weights", "mfx_acnet_forward",
-                   "mfx_acnet_act_rollout"):
+                   "mfx_acnet_act_rollout", "mfx_acnet_set_input_support", "mfx_acnet_input_support_size"):
             getattr(L, fn).restype = ctypes.c_int
         self._L = L
         self.blob_n, self.offsets = acnet_layout(self.V, self.F, self.A, self.use_mf)
         hdl = _P()
         check(L.mfx_acnet_create(self.V, self.F, self.A, int(self.use_mf), ctypes.byref(hdl)), "mfx_acnet_create")
         self.handle = hdl
-        self._rows = None
+        self._rows = {}
+        self._support = None
 
     def __del__(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
@@ -247,6 +256,26 @@ class ACNetHIP:
         check(self._L.mfx_acnet_set_weights(self.handle, _ptr(self._blob), ctypes.c_size_t(self.blob_n), _stream()),
               "mfx_acnet_set_weights")
         return self
+
+    def set_input_support(self, mask):
+        """mask: uint8/bool [V], 1 where the view can be non-zero (e.g. BattleBatch.view_support), or None for the
+        dense order.  Later forwards run the view layer over the supported inputs only -- the same results bit for
+        bit while the view is zero elsewhere, which the caller guarantees (the engine's observation buffers are)."""
+        if mask is None:
+            check(self._L.mfx_acnet_set_input_support(self.handle, None, 0, _stream()), "mfx_acnet_set_input_support")
+            self._support = None
+            return self
+        m = np.ascontiguousarray(np.asarray(mask, dtype=np.uint8).reshape(-1))
+        check(self._L.mfx_acnet_set_input_support(self.handle, m.ctypes.data_as(ctypes.c_void_p), int(m.size),
+                                                  _stream()), "mfx_acnet_set_input_support")
+        self._support = m.copy()
+        return self
+
+    def input_support_size(self):
+        """Inputs the view layer runs over (0: the dense order)."""
+        k = ctypes.c_int()
+        check(self._L.mfx_acnet_input_support_size(self.handle, ctypes.byref(k)), "mfx_acnet_input_support_size")
+        return k.value
 
     def forward(self, view, feature, prob=None, want_policy=True, want_value=False, want_act=True, seed=0, step=0):
         """view [n, ...] (flattened to V), feature [n, F], prob [n, A] (the MF value head) float32 CUDA tensors
@@ -272,13 +301,22 @@ class ACNetHIP:
     def act(self, view, feature, seed=0, step=0):
         return self.forward(view, feature, want_policy=False, seed=seed, step=step)[2]
 
-    def act_rollout(self, eng, group, seed, step):
+    def act_rollout(self, eng, group, seed, step, support=True):
         """Sampled actions of group `group` of a BattleBatch rollout from its current observation buffers,
         written into the rollout's action buffer [E][G][rowcap] (live rows; row j of env e drawn with (seed,
-        step, group, e * rowcap + j)).  Nothing is read back to the host."""
+        step, group, e * rowcap + j)).  Nothing is read back to the host.  support: run the view layer over the
+        inputs the engine's view can make non-zero only (BattleBatch.view_support; bit-identical).  The row-list
+        scratch is per engine, so engines on different streams may share this network."""
         E, rc, G = eng.n_envs, eng.rowcap, len(eng.handles)
-        if self._rows is None or self._rows.numel() < E * rc + 1:
-            self._rows = torch.empty(E * rc + 1, dtype=torch.int32, device="cuda")
+        if support:
+            m = eng.view_support(group)
+            if self._support is None or not np.array_equal(self._support, m):
+                self.set_input_support(m)
+        elif self._support is not None:
+            self.set_input_support(None)
+        rows = self._rows.get(id(eng))
+        if rows is None or rows.numel() < rows_scratch(E, rc):
+            rows = self._rows[id(eng)] = torch.empty(rows_scratch(E, rc), dtype=torch.int32, device="cuda")
         ptr = {}
         for name in ("view", "feature", "group_num", "actions"):
             p, nb = _P(), ctypes.c_size_t()
@@ -286,7 +324,7 @@ class ACNetHIP:
                                                           else 0, ctypes.byref(p), ctypes.byref(nb)), "rollout_buffer")
             ptr[name] = p
         check(self._L.mfx_acnet_act_rollout(self.handle, ptr["view"], ptr["feature"], ptr["group_num"], int(E), int(G),
-                                            int(group), int(rc), _P(self._rows.data_ptr()),
-                                            _P(self._rows.data_ptr() + 4 * E * rc), ptr["actions"],
+                                            int(group), int(rc), _P(rows.data_ptr()),
+                                            _P(rows.data_ptr() + 4 * E * rc), ptr["actions"],
                                             ctypes.c_uint32(seed & 0xFFFFFFFF), ctypes.c_uint32(step & 0xFFFFFFFF),
                                             _P(eng.stream_handle())), "mfx_acnet_act_rollout")

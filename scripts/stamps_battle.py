@@ -2,7 +2,9 @@
 
     MAGENT_LIB=.../build/libmagent_stamps.so python scripts/stamps_battle.py --envs 4096
 Reports median / mean cycles per phase over envs for a few steady-state steps (shares only:
-the stamp build's barriers forbid overlaps the real kernel has)."""
+the stamp build's barriers forbid overlaps the real kernel has).  Shader-clock (s_memtime) deltas within one env's
+processing only: the stamp build records no wall-clock (s_memrealtime) slots, so it says nothing about residency or
+launch spans (scripts/timeline_rollout.py measures those)."""
 import argparse
 import ctypes
 import os
@@ -32,32 +34,22 @@ eng.rollout_step(400)
 torch.cuda.synchronize()
 acc = []
 raw = []
-conc = []
-inst = []
 sub = []
 for t in range(a.steps):
     buf.zero_()
     eng.rollout_step(1)
     torch.cuda.synchronize()
     st = buf.view(a.envs, 32).cpu().numpy().astype(np.int64)
+    done = (st[:, 0] > 0) & (st[:, 10] > st[:, 0])      # envs whose stamps 0 .. 10 all landed this launch
+    st = st[done]
     raw.append(st)
     acc.append(np.diff(st[:, :11], axis=1))
-    sub.append(np.stack([st[:, 13] - st[:, 0], st[:, 1] - st[:, 13], 10 * (st[:, 11] - st[:, 14])], 1))
-    rt0, rt1 = st[:, 11], st[:, 12]            # s_memrealtime, 100 MHz
-    span = rt1.max() - rt0.min()
-    fr = [0.02, 0.1, 0.3, 0.5, 0.7, 0.9, 0.98]
-    inst.append([((rt0 <= rt0.min() + f * span) & (rt1 >= rt0.min() + f * span)).sum() for f in fr])
-    conc.append(((rt1 - rt0).sum() / span, span / 100.0, (st[:, 10] - st[:, 0]).sum() / (rt1 - rt0).sum() / 100.0))
+    sub.append(np.stack([st[:, 13] - st[:, 0], st[:, 1] - st[:, 13]], 1))
 d = np.concatenate(acc)
 tot = d.sum(1)
-print("env lifetime (stamp 0 -> 10): median %d cycles, mean %d" % (np.median(tot), tot.mean()))
-c = np.array(conc)
-print("envs in flight (mean over the launch) %.0f; launch span %.0f us; shader clock %.2f GHz"
-      % (c[:, 0].mean(), c[:, 1].mean(), c[:, 2].mean()))
-print("  envs resident at 2/10/30/50/70/90/98%% of the launch:", np.array(inst).mean(0).round().astype(int).tolist())
+print("env lifetime (stamp 0 -> 10): median %d cycles, mean %d (%d env-steps)" % (np.median(tot), tot.mean(), len(tot)))
 sb = np.concatenate(sub)
-print("  install split: LDS stores + barrier mean %d, prefetch issue + barrier mean %d; loop top -> stamp 0 "
-      "mean %d ns" % tuple(sb.mean(0)))
+print("  install split: LDS stores + barrier mean %d cycles, prefetch issue + barrier mean %d cycles" % tuple(sb.mean(0)))
 R = np.concatenate(raw)
 parts = np.stack([R[:, 17] - R[:, 5], R[:, 18] - R[:, 17], R[:, 15] - R[:, 18], R[:, 19] - R[:, 15],
                   R[:, 6] - R[:, 19]], 1)

@@ -8,8 +8,13 @@ coalesced stream (MI355X_MICROARCH.md, HBM) so it is doubled; WRITE_SIZE is exac
 Only k_rollout dispatches of the timed part are used (the last `timed_launches` launches of the trace,
 the last `pmc_launches` of each PMC pass); one launch runs `substeps` steps of every env."""
 import csv
+import hashlib
 import json
+import os
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "mean-field-multi-agent-reinforcement-learning_amd", "build", "libmagent.so")
 
 
 def per_launch(path, counter, n):
@@ -28,6 +33,8 @@ f_kib, nf = per_launch(fetch + "/run_counter_collection.csv", "FETCH_SIZE", npmc
 w_kib, nw = per_launch(write + "/run_counter_collection.csv", "WRITE_SIZE", npmc)
 res = {
     "envs": int(envs),
+    # the library build the counters were collected on (bench.py attaches them only to lines of the same build)
+    "lib_sha16": hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16],
     "substeps": sub,
     "kernel_stats": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")} for r in stats],
     "k_rollout_timed_avg_ns": sum(dur[-timed:]) / len(dur[-timed:]),

@@ -43,7 +43,7 @@ for L in range(a.launches):
     ev[1].record()
     torch.cuda.synchronize()
     st = buf.view(E, 32).cpu().numpy().astype(np.int64)
-    t0, t1, wg, n0 = st[:, 11], st[:, 12], st[:, 28], st[:, 29]
+    t0, t1, wg, n0 = st[:, 11], st[:, 12], st[:, 27], st[:, 29]
     base = t0.min()
     t0, t1 = (t0 - base) / 100.0, (t1 - base) / 100.0          # us
     span = t1.max()

@@ -74,3 +74,27 @@ def test_dropin_rejects_unsupported_config(built):
     env = magent.GridWorld(cfg, lib=magent.load_library(built))
     with pytest.raises(magent.EngineError, match="align"):
         env.reset()
+
+
+def test_battle_view_support_without_gpu(built):
+    """mfx_battle_view_support: the Battle view (13 x 13 x 7) can be non-zero in every channel of the 113 cells of
+    the radius-6 view circle and in the two minimap channels (3, 6) of every cell; nothing else is ever written
+    (Map.cc:130-218, GridWorld.cc:396-409).  No device work: the parameters compile on the host."""
+    import numpy as np
+    import magent
+    env = magent.GridWorld("battle", map_size=64, lib=magent.load_library(built))
+    h = env.get_handles()
+    dll = env._lib.dll
+    dll.mfx_battle_view_support.restype = ctypes.c_int
+    for g in range(2):
+        m = np.zeros(13 * 13 * 7, dtype=np.uint8)
+        assert dll.mfx_battle_view_support(env.game, g, m.ctypes.data_as(ctypes.c_void_p), m.size) == 0
+        m = m.reshape(13, 13, 7)
+        y, x = np.mgrid[-6:7, -6:7]
+        circle = (x * x + y * y <= 36).astype(np.uint8)
+        assert circle.sum() == 113
+        for ch in range(7):
+            assert np.array_equal(m[:, :, ch], np.ones_like(circle) if ch in (3, 6) else circle), ch
+        assert int(m.sum()) == 903
+    bad = np.zeros(10, dtype=np.uint8)
+    assert dll.mfx_battle_view_support(env.game, 0, bad.ctypes.data_as(ctypes.c_void_p), bad.size) != 0

@@ -9,6 +9,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+
 
 def _free_port():
     s = socket.socket()
@@ -108,3 +110,41 @@ def test_bench_refuses_more_rccl_ranks_than_gpus():
     assert bench.rank_device(3, 2, 2, "gloo") == (0, 2)
     with pytest.raises(RuntimeError):
         bench.rank_device(1, 0, 0, "nccl")
+
+
+def _ising_worker(rank, world, port, R, T, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import numpy as np
+    import ising_oracle
+    from mfrl_amd.dist import reduce_ising, replica_block
+    r0, n = replica_block(R, world, rank)
+    res = [ising_oracle.mfq(16, 0.8, T, seed=13 + r0 + r) for r in range(n)]
+    final = [x["order"][-1] for x in res]
+    steps = np.array([x["steps"] for x in res])
+    out[rank] = (r0, n, reduce_ising(final, steps), final)
+    dist.destroy_process_group()
+
+
+def test_two_rank_ising_replica_sharding():
+    """Ising replicas over 2 gloo ranks (scripts/bench_ising.py --gpus 2): the blocks cover the replica range once
+    (replica r on seed 13 + r wherever it runs), and the one all-reduce of (sum of final order parameters, sum of
+    steps, replicas) equals the single-rank sum over the same replicas (main_MFQ_Ising.py:138-156's order
+    parameter, here from the numpy oracle)."""
+    import numpy as np
+    import ising_oracle
+    from mfrl_amd.dist import replica_block
+    R, T, world = 7, 400, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_ising_worker, args=(world, _free_port(), R, T, out), nprocs=world, join=True)
+    blocks = sorted((out[r][0], out[r][1]) for r in range(world))
+    assert blocks == [replica_block(R, world, r) for r in range(world)] == [(0, 4), (4, 3)]
+    single = [ising_oracle.mfq(16, 0.8, T, seed=13 + r) for r in range(R)]
+    want = [sum(x["order"][-1] for x in single), float(sum(x["steps"] for x in single)), float(R)]
+    got = out[0][2]
+    assert got == out[1][2]
+    assert got[1:] == want[1:]
+    assert abs(got[0] - want[0]) <= 1e-12 * max(1.0, abs(want[0]))
+    finals = out[0][3] + out[1][3]
+    assert np.array_equal(np.array(finals), np.array([x["order"][-1] for x in single]))

@@ -193,3 +193,46 @@ def test_device_stream_many_replicas_match_oracle():
         assert int(got["steps"][r]) == ref["steps"]
         assert got["order"][r, :ref["steps"]].tobytes() == ref["order"].tobytes()
         assert got["q"][r].tobytes() == ref["q"].tobytes()
+
+
+def test_device_stream_multi_pass_episodes_match_oracle(monkeypatch):
+    """The word streams of many replicas in several generation passes (MFX_ISING_PASS_GB=1: ~119 replicas of 400
+    agents x 700 steps x 2 episodes per pass, 512 replicas = 5 passes: the two-slot pipeline, pass p + 2 produced
+    once pass p released its slot) with 2 episodes per replica on one stream: sampled replicas of every pass,
+    both episodes, against the numpy oracle (mfq_episodes, seed 13 + r) bit for bit."""
+    from mfrl_amd.ising import IsingLattice
+    monkeypatch.setenv("MFX_ISING_PASS_GB", "1")
+    R, T = 512, 700
+    got = IsingLattice(400, R).run_mfq_stream(T, 0.8, seed=13, episodes=2)
+    for r in (0, 118, 119, 300, R - 1):
+        ref = ising_oracle.mfq_episodes(400, 0.8, T, 2, seed=13 + r)
+        for k in range(2):
+            S = ref[k]["steps"]
+            assert int(got[k]["steps"][r]) == S, (r, k)
+            assert got[k]["order"][r, :S].tobytes() == ref[k]["order"].tobytes(), (r, k)
+            np.testing.assert_array_equal(got[k]["n_up"][r, :S], ref[k]["n_up"])
+            assert got[k]["q"][r].tobytes() == ref[k]["q"].tobytes(), (r, k)
+
+
+def test_device_stream_refuses_word_offsets_past_32_bits():
+    """episodes x T x 4 N words per replica past 2^32 cannot be addressed by the 32-bit per-step offsets: the call
+    fails loudly before any allocation, and run_mfq_episodes takes the host stream for such runs."""
+    import magent
+    from mfrl_amd import ising
+    lat = ising.IsingLattice(400, 1)
+    assert ising.stream_words(400, 10000, 300) * 1 > 2 ** 32
+    with pytest.raises(magent.EngineError, match="32-bit"):
+        lat.run_mfq_stream(10000, 0.8, episodes=300)
+    assert 4 * ising.stream_words(400, 10000, 300) > ising.STREAM_MAX_BYTES
+
+
+def test_episodes_host_fallback_matches_reference_mode(monkeypatch):
+    """run_mfq_episodes past STREAM_MAX_BYTES per replica runs the host stream: the same episodes bit for bit."""
+    from mfrl_amd import ising
+    ref = ising.run_mfq_episodes(36, 0.8, 900, 3, seed=5)
+    monkeypatch.setattr(ising, "STREAM_MAX_BYTES", 1024)
+    got = ising.run_mfq_episodes(36, 0.8, 900, 3, seed=5)
+    for a, b in zip(ref, got):
+        assert int(a["steps"][0]) == int(b["steps"][0])
+        assert a["q"].tobytes() == b["q"].tobytes()
+        assert a["order"][0, :int(a["steps"][0])].tobytes() == b["order"][0, :int(b["steps"][0])].tobytes()

@@ -251,6 +251,52 @@ def test_acnet_forward_matches_torch_module(use_mf):
     assert abs(float(p_of.mean()) - float((pol * pol).sum(1).mean())) < 0.01
 
 
+@pytest.mark.parametrize("use_mf", [False, True])
+def test_acnet_input_support_is_bit_identical(use_mf):
+    """The view layer over the engine's view support only (mfx_acnet_set_input_support with
+    mfx_battle_view_support: 903 of the 1,183 inputs, the rest never written by the observation) gives the dense
+    forward's policy, value and draw bit for bit, on bench-shape rollout rows -- whose unsupported inputs are
+    checked to be exactly zero -- and on random rows zeroed outside a random support (other gaps in the packed
+    order, ragged n)."""
+    import torch
+    from mfrl_amd.battle import BattleBatch
+    from mfrl_amd.policy import ACNetHIP
+    net = _acnet(use_mf, 51 + use_mf)
+    view, feat, prob = _rollout_obs(E=2048, steps=45)
+    n = view.shape[0]
+    mask = BattleBatch(64, 4, stream=torch.cuda.current_stream()).view_support(0)
+    assert int(mask.sum()) == 903
+    off = torch.from_numpy(mask == 0).cuda()
+    assert not view.reshape(n, -1)[:, off].any()              # the observation never writes them
+    hip = ACNetHIP((13, 13, 7), (34,), 21, use_mf).load(net)
+    dense = hip.forward(view, feat, prob, want_value=True, seed=9, step=2)
+    hip.set_input_support(mask)
+    assert hip.input_support_size() == 903
+    packed = hip.forward(view, feat, prob, want_value=True, seed=9, step=2)
+    torch.cuda.synchronize()
+    for a, b in zip(dense, packed):
+        assert torch.equal(a, b)
+    # an arbitrary support; support cleared again -> dense
+    rng = np.random.RandomState(3)
+    rmask = (rng.rand(1183) < 0.55).astype(np.uint8)
+    m = 517
+    v = torch.randn(m, 1183, device="cuda") * torch.from_numpy(rmask).cuda().float()
+    hip.set_input_support(rmask)
+    assert hip.input_support_size() == int(rmask.sum())
+    packed = hip.forward(v, feat[:m], prob[:m], want_value=True, seed=1, step=7)
+    hip.load(_acnet(use_mf, 61))                              # new weights: the packed image is remade
+    packed2 = hip.forward(v, feat[:m], prob[:m], want_value=True, seed=1, step=7)
+    hip.set_input_support(None)
+    assert hip.input_support_size() == 0
+    dense2 = hip.forward(v, feat[:m], prob[:m], want_value=True, seed=1, step=7)
+    hip.load(net)
+    dense = hip.forward(v, feat[:m], prob[:m], want_value=True, seed=1, step=7)
+    torch.cuda.synchronize()
+    for a, b, c, d in zip(dense, packed, dense2, packed2):
+        assert torch.equal(a, b) and torch.equal(c, d)
+    assert not torch.equal(dense[0], dense2[0])
+
+
 def test_acnet_forward_small_and_ragged_batches():
     """n = 1, 15, 17, 63, 65 give the rows (policy, value, draw) a full batch gives them."""
     import torch
@@ -361,3 +407,30 @@ def test_mfac_policy_rollout_matches_oracle(monkeypatch):
         obs = nxt
     eng.rollout_check()
     assert restarts >= E
+
+
+@pytest.mark.parametrize("E", [1, 63, 64, 65, 8192, 131072])
+def test_rollout_rows_match_numpy(E):
+    """The compact row list of act_rollout (two-level scan over 64-env chunks) at up to the bench's
+    131072 envs: every row index and the count against numpy, counts capped at rowcap, empty envs included."""
+    import ctypes
+    import torch
+    from mfrl_amd import check, lib
+    from mfrl_amd.policy import rows_scratch
+    G, rowcap = 2, 128
+    rng = np.random.RandomState(E)
+    counts = rng.randint(0, rowcap + 40, size=(E, G)).astype(np.int32)
+    counts[rng.rand(E) < 0.1, 1] = 0
+    d_counts = torch.from_numpy(counts).cuda()
+    buf = torch.full((rows_scratch(E, rowcap),), -7, dtype=torch.int32, device="cuda")
+    L = lib()
+    L.mfx_rollout_rows.restype = ctypes.c_int
+    P = ctypes.c_void_p
+    check(L.mfx_rollout_rows(P(d_counts.data_ptr()), E, G, 1, rowcap, P(buf.data_ptr()),
+                             P(buf.data_ptr() + 4 * E * rowcap), P(torch.cuda.current_stream().cuda_stream)),
+          "mfx_rollout_rows")
+    got = buf.cpu().numpy()
+    n = np.minimum(counts[:, 1], rowcap)
+    want = np.concatenate([e * rowcap + np.arange(k) for e, k in enumerate(n)]) if n.sum() else np.zeros(0, np.int32)
+    assert got[E * rowcap] == n.sum()
+    assert np.array_equal(got[:len(want)], want)
