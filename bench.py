@@ -119,9 +119,11 @@ def parse(argv=None):
     ap.add_argument("--no-ceiling", dest="ceiling", action="store_false",
                     help="skip the measured write ceiling after the clock (roofline.measured_peak)")
     ap.add_argument("--split", type=int, default=None,
-                    help="learned-policy modes: the envs as this many engines on their own HIP streams (overlap; "
-                         "default 2 for mfac -- 1.016e8 -> 1.051e8 agent-steps/s on one box, profiles/r06_mfac.txt -- "
-                         "1 for qnet)")
+                    help="the envs as this many engines on their own HIP streams, so one engine's launch overlaps "
+                         "another's (default: rush 2 for 64x64 batches of 2048-16384 envs per GPU -- the launch tails "
+                         "at under 16 envs per workgroup: 8192 envs 0.60 -> 0.67-0.87 by box, 16384 0.64 -> 0.73, "
+                         "profiles/r06_split.txt -- else 1; mfac 2 -- 1.016e8 -> 1.051e8 agent-steps/s, "
+                         "profiles/r06_mfac.txt; qnet 1)")
     ap.add_argument("--dense-view", action="store_true",
                     help="mfac: the view layer over all 1,183 inputs (A/B; default: the engine's view support)")
     ap.add_argument("--check-envs", type=int, default=8,
@@ -129,7 +131,7 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     if a.envs is None and a.total_envs is None and a.policy != "rush":
         a.envs = 8192                 # the network forward bounds these modes (1.2 / 3.4 MFLOP per agent-step)
-    if a.split is None:
+    if a.split is None and a.policy != "rush":
         a.split = 2 if a.policy == "mfac" else 1
     if a.envs is None and a.total_envs is None:
         # 64x64: 131072 envs per GPU (~160 GB of observation buffers, 56 % of the HBM) -- a launch has a fixed
@@ -339,40 +341,45 @@ def run_cpu_baseline(seconds, map_size, agents, procs=None):
 
 
 # ----------------------------------------------------------------------------- self-check
-def run_check(eng, args, E, placement, seed, world):
-    """Replay args.check_envs sampled envs of this rank's batch on the C oracle from rollout_init through
-    the preparation, warmup and timed steps (tests/rollout_check.py); all ranks' verdicts reduced."""
+def run_check(engs, args, sizes, placement, seeds, world):
+    """Replay args.check_envs sampled envs of this rank's batch (spread over its engines) on the C oracle from
+    rollout_init through the preparation, warmup and timed steps (tests/rollout_check.py), one of them on the
+    reference engine itself as well; all ranks' verdicts reduced."""
     if args.check_envs <= 0:
         return None
     import torch
     import torch.distributed as dist
     import rollout_check as rc
     steps = args.max_steps + args.warmup + args.steps            # every step since rollout_init
-    envs = rc.sample_envs(E, args.check_envs)
     ref_lib = os.path.join(REPO, "oracle", "_ref", "libmagent_ref.so")
-    ref_env = envs[len(envs) // 2] if os.path.exists(ref_lib) else None
     t = time.perf_counter()
     err = None
-    bad_ref = []
-    try:
-        chk = rc.RolloutChecker(eng, args.map, placement, envs, args.max_steps, True, seed, 0.2)
-        bad = chk.check(steps)
-        if ref_env is not None:
-            # one of the sampled envs replayed on the reference engine itself as well (VERDICT r4 next 2)
-            ref = rc.RolloutChecker(eng, args.map, placement, [ref_env], args.max_steps, True, seed, 0.2, lib=ref_lib)
-            bad_ref = ref.check(steps)
-    except Exception as x:                  # a device / queue error word (rollout_check) or a failed read
-        bad, err = ["%s: %s" % (type(x).__name__, x)], True
-    bad = bad + ["reference build: " + b for b in bad_ref]
+    bad, sample, ref_env = [], [], None
+    H = len(engs)
+    for h, (eng, E, seed) in enumerate(zip(engs, sizes, seeds)):
+        envs = rc.sample_envs(E, max(1, args.check_envs // H + (1 if h < args.check_envs % H else 0)))
+        sample.append(envs)
+        try:
+            chk = rc.RolloutChecker(eng, args.map, placement, envs, args.max_steps, True, seed, 0.2)
+            bad += [("engine %d: " % h if H > 1 else "") + b for b in chk.check(steps)]
+            if h == 0 and os.path.exists(ref_lib):
+                # one of the sampled envs replayed on the reference engine itself as well (VERDICT r4 next 2)
+                ref_env = envs[len(envs) // 2]
+                ref = rc.RolloutChecker(eng, args.map, placement, [ref_env], args.max_steps, True, seed, 0.2,
+                                        lib=ref_lib)
+                bad += ["reference build: " + b for b in ref.check(steps)]
+        except Exception as x:              # a device / queue error word (rollout_check) or a failed read
+            bad, err = bad + ["%s: %s" % (type(x).__name__, x)], True
+    n_local = sum(len(x) for x in sample)
     ok = torch.tensor([0.0 if bad else 1.0], dtype=torch.float64, device="cuda")
-    n = torch.tensor([float(len(envs))], dtype=torch.float64, device="cuda")
+    n = torch.tensor([float(n_local)], dtype=torch.float64, device="cuda")
     nref = torch.tensor([0.0 if ref_env is None else 1.0], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         dist.all_reduce(n)
         dist.all_reduce(nref)
-    return {"ok": bool(ok.item() == 1.0), "envs": int(n.item()), "envs_per_rank": len(envs), "steps": steps,
-            "sample_rank0": envs, "path": eng.rollout_path() if err is None else None,
+    return {"ok": bool(ok.item() == 1.0), "envs": int(n.item()), "envs_per_rank": n_local, "steps": steps,
+            "sample_rank0": sample[0] if H == 1 else sample, "path": engs[0].rollout_path() if err is None else None,
             "reference_envs": int(nref.item()), "reference_env_rank0": ref_env,
             "what": "each sampled env replayed from rollout_init on the C oracle (oracle/battle_oracle.c) with a "
                     "host restatement of the device rush policy, and one of them (reference_env_rank0) also on the "
@@ -564,32 +571,61 @@ def main():
     stream = torch.cuda.current_stream()
     left, right = bd.block_positions(args.map, args.agents // 2)
     from mfrl_amd.dist import env_seed, reduce_stats, reduce_timing
-    eng = BattleBatch(args.map, E, stream=stream)
-    eng.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=env_seed(1234, rank))
+    # the envs as H engines on H HIP streams (--split; default: 2 for k_rollout batches of under 16 envs per
+    # workgroup): one engine's launch tail runs beside the other's launch (profiles/r06_split.txt)
+    H = args.split if args.split is not None else (
+        2 if args.map * args.map <= 64 * 64 and 2048 <= E <= 16384 and args.policy == "rush" else 1)
+    H = max(1, min(H, E))
+    sizes = [E // H + (1 if h < E % H else 0) for h in range(H)]
+    streams = [stream] + [torch.cuda.Stream() for _ in range(H - 1)]
+    seeds = [env_seed(1234, rank) + 104729 * h for h in range(H)]
+    engs = []
+    for h in range(H):
+        e = BattleBatch(args.map, sizes[h], stream=streams[h])
+        e.rollout_init([left, right], max_steps=args.max_steps, eps=0.2, seed=seeds[h])
+        e.rollout_substeps(max(0, args.substeps))
+        engs.append(e)
+    eng = engs[0]
     path = eng.rollout_path()               # the kernels rollout_step runs (chosen by the engine)
     grid, lds = eng.rollout_info()          # persistent grid, LDS bytes per workgroup
-    eng.rollout_substeps(max(0, args.substeps))
     S = eng.get_substeps()                  # (0: the engine's choice for this path and batch)
     big = path in ("k_rollout_bigq", "k_observe_items+k_rollout_big")   # large envs, state in HBM
-    steps_buf = torch.zeros(E, dtype=torch.int64, device="cuda")
-    stats_buf = torch.zeros(E * 4, dtype=torch.float64, device="cuda")
+    steps_buf = [torch.zeros(n, dtype=torch.int64, device="cuda") for n in sizes]
+    stats_buf = [torch.zeros(n * 4, dtype=torch.float64, device="cuda") for n in sizes]
+
+    def join():                             # the main stream waits for every engine's stream
+        for st in streams[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            stream.wait_event(ev)
+
+    def fork():                             # every engine's stream waits for the main stream
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        for st in streams[1:]:
+            st.wait_event(ev)
 
     def agent_steps():
-        eng.rollout_copy("agent_steps", steps_buf)
-        return steps_buf.sum()
+        for e, b in zip(engs, steps_buf):
+            e.rollout_copy("agent_steps", b)
+        join()
+        return sum(b.sum() for b in steps_buf)
 
     def stats():
-        eng.rollout_copy("stats", stats_buf)
-        return stats_buf.view(E, 4)
+        for e, b in zip(engs, stats_buf):
+            e.rollout_copy("stats", b)
+        join()
+        return torch.cat(stats_buf).view(E, 4)
 
     # input preparation: run one episode cap of steps so that the staggered envs hold every
     # phase of an episode (early fights with ~256 agents ... late game with few survivors)
-    eng.rollout_step(args.max_steps + args.warmup)
+    for e in engs:
+        e.rollout_step(args.max_steps + args.warmup)
     torch.cuda.synchronize()
 
-    # launches of the timed region: S steps each (the last one the remainder); HIP events on the engine's
-    # stream around the whole region (an event pair around every launch put two timestamp packets between
-    # consecutive launches: at 8192 envs x 2 steps per launch ~5 % of the wall time went to them)
+    # launches of the timed region: S steps each (the last one the remainder); HIP events on the main stream around
+    # the whole region, the engines' streams forked from and joined into it (an event pair around every launch put
+    # two timestamp packets between consecutive launches: at 8192 envs x 2 steps per launch ~5 % of the wall time)
     chunks = [min(S, args.steps - k) for k in range(0, args.steps, S)]
     # one event pair per run of launches between collectives (one run at world 1): the roofline's kernel time
     # leaves the statistics' all-reduce and the wait for other ranks out
@@ -605,15 +641,19 @@ def main():
         if not segs or segs[-1][1] is not None:
             segs.append([torch.cuda.Event(enable_timing=True), None])
             segs[-1][0].record(stream)
-        eng.rollout_step(n)
+            fork()
+        for e in engs:
+            e.rollout_step(n)
         done_steps += n
         # episode statistics -> RCCL all-reduce, once per episode batch (an episode cap of steps) and at
         # the end of the timed window: the only collective
         if world > 1 and (done_steps // args.max_steps != (done_steps - n) // args.max_steps or k == len(chunks) - 1):
+            join()
             segs[-1][1] = torch.cuda.Event(enable_timing=True)
             segs[-1][1].record(stream)
             red = reduce_stats(stats())
     if segs[-1][1] is None:
+        join()
         segs[-1][1] = torch.cuda.Event(enable_timing=True)
         segs[-1][1].record(stream)
     torch.cuda.synchronize()
@@ -624,12 +664,11 @@ def main():
     if red is None:                  # one rank: the same statistics, reduced after the clock
         red = reduce_stats(stats())
     red = red.tolist()
-    # the mean launch of the timed region (its launches back to back on the stream between collectives: the runs'
-    # time / their launch count)
+    # the mean launch (round of H concurrent launches) of the timed region: the runs' time / their launch count
     kernel_ms = sum(a.elapsed_time(b) for a, b in segs) / len(chunks)
     local_units = float((a1 - a0).item())
     elapsed, total_units = reduce_timing(t1 - t0, local_units, "cuda")
-    check = run_check(eng, args, E, [left, right], env_seed(1234, rank), world)
+    check = run_check(engs, args, sizes, [left, right], seeds, world)
     # the measured write ceiling of this GPU (after the check: it overwrites the view buffer)
     ceiling = measure_ceiling(eng, BYTES_PER_AGENT_STEP * local_units / len(chunks)) if args.ceiling else None
     if rank == 0:
@@ -645,7 +684,7 @@ def main():
                 pm = json.load(f)
             # counters are attached only when they were collected on this build of the library at this shape
             if (pm.get("envs") == E and pm.get("map", MAP) == args.map and pm.get("substeps", 1) == S
-                    and pm.get("lib_sha16") == lib_sha16()):
+                    and pm.get("engines", 1) == H and pm.get("lib_sha16") == lib_sha16()):
                 traffic = pm.get("hbm_bytes_per_launch", pm.get("hbm_bytes_per_step"))
         strong = args.total_envs is not None
         kern = {"k_rollout_obs+k_rollout": "k_rollout"}.get(path, path)
@@ -666,9 +705,12 @@ def main():
                            ("%d envs over %d ranks on %d GPU(s)" % (args.total_envs, world, n_gpus))) if strong else
                           "%d envs per GPU" % E if n_gpus == world else "%d envs per rank" % E,
                           args.max_steps,
-                          ("%s, %d steps per launch" % (path, S_run)) if big else
-                          ("fused step" if S_run == 1 else "fused step, %d consecutive steps per launch" % S_run)),
+                          (("%s, %d steps per launch" % (path, S_run)) if big else
+                           ("fused step" if S_run == 1 else "fused step, %d consecutive steps per launch" % S_run)) +
+                          ("; the envs as %d engines of %s envs on %d HIP streams" % (H, "/".join(map(str, sorted(set(sizes)))), H)
+                           if H > 1 else "")),
                        "map": args.map, "agents": args.agents, "envs_per_gpu": E, "steps_per_launch": S_run,
+                       "engines": H,
                        # agents placed per episode start vs the live agents an env-step actually carries (the
                        # unit counts live agents; battles thin the armies, staggered episodes mix all phases)
                        "live_agents_per_env_step": local_units / (args.steps * E),
@@ -679,8 +721,11 @@ def main():
                          "kernel": kern, "kernel_ms": kernel_ms,
                          "kernel_ms_is": "mean launch duration: HIP events on the launch stream around the timed "
                                          "region's %d launch(es) (%d run(s) of back-to-back launches between "
-                                         "collectives), / their count; %g step(s) per launch"
-                                         % (len(chunks), len(segs), steps_per_timed_launch),
+                                         "collectives), / their count; %g step(s) per launch%s"
+                                         % (len(chunks), len(segs), steps_per_timed_launch,
+                                            "; each launch here is %d concurrent launches, one per engine and stream "
+                                            "(the events on the main stream, the engines' streams forked from and "
+                                            "joined into it)" % H if H > 1 else ""),
                          "bytes_per_unit": BYTES_PER_AGENT_STEP, "units_per_launch": units_per_launch,
                          "measured_peak": ceiling["peak"] if ceiling else None,
                          "frac_measured": achieved / ceiling["peak"] if ceiling else None,

@@ -107,8 +107,8 @@ constexpr int kHeF = 36;
 constexpr size_t kAcnetLdsSmem = kQHeadSmem + (size_t)kHeF * kAH * 4;
 constexpr size_t kAcnetImgLdsSmem = kImgSmem + (size_t)kHeF * kAH * 4 + 3 * 1024 * 4;   // + the view ring: 80 KB
 
-// kImg: the layers run wg_gemm_i over the weight images (direct-to-LDS staging; the default), else wg_gemm_t (A/B:
-// MFX_ACNET_IMG=0).  GEMM<MT, NCH, kZero>(block, image, K, v_at, acc) picks the form.
+// kImg: the layers run wg_gemm_i over the weight images (direct-to-LDS staging; made by set_weights), else
+// wg_gemm_t.  GEMM<MT, NCH, kZero>(block, image, K, v_at, acc) picks the form.
 template <typename PT, bool kMF, bool kHeLds, bool kImg, bool kPack = false>
 __global__ void __launch_bounds__(256, kHeLds ? 2 : 1) k_acnet(ACNetDev p, const float* __restrict__ view, size_t view_ld,
                                                   const float* __restrict__ feat, size_t feat_ld,
@@ -584,14 +584,9 @@ static int acnet_run(ACNetHandle* q, const float* view, size_t view_ld, const fl
     if (q->dev.use_mf && value && !prob) return fail("acnet: the mean-field value head needs prob");
     // persistent workgroups: as many as the CUs hold at once (two per CU with h_emb in LDS), at most one per tile
     int grid = (n + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
-    const char* hl = getenv("MFX_ACNET_HE_LDS");                    // A/B only: 0 = h_emb held in registers
-    const bool lds = q->dev.Fp <= kHeF && !(hl && atoi(hl) == 0);
-    const char* il = getenv("MFX_ACNET_IMG");                       // A/B only: 0 = wg_gemm_t's register staging
-    const bool img = q->imaged && !(il && atoi(il) == 0);
-    {
-        const char* pl = getenv("MFX_ACNET_PERSIST");               // A/B only: 0 = one workgroup per tile
-        if (!(pl && atoi(pl) == 0)) grid = std::min(grid, (lds ? 2 : 1) * device_cus());
-    }
+    const bool lds = q->dev.Fp <= kHeF;                             // (wider features: h_emb held in registers)
+    const bool img = q->imaged;
+    grid = std::min(grid, (lds ? 2 : 1) * device_cus());
 #define MFX_ACNET_LAUNCH1(PT, MF, LDS, IMG, PK, PB)                                                                     \
     k_acnet<PT, MF, LDS, IMG, PK><<<grid, 256, IMG && LDS ? kAcnetImgLdsSmem : (LDS ? kAcnetLdsSmem : kQHeadSmem),     \
                                     st>>>(q->dev, view, view_ld, feat, feat_ld, PB, prob_ld, rm, n, d_n, policy, value,   \

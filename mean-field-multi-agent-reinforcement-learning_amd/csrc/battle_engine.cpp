@@ -1260,12 +1260,6 @@ public:
             ra.renumber = 0;
             ra.lds_step = 0;
             ra.few_pipe = 0;
-            {
-                // A/B only: 0 = the round-3 queue (consecutive ranks, claims two envs ahead), 2 = tiers without the
-                // restart-aware filing weights
-                const char* qt = getenv("MFX_QUEUE_TIERS");
-                ra.queue_tiers = qt ? std::min(std::max(atoi(qt), 0), 2) : 1;
-            }
             if (ro_big) {
                 ro_grid = E;
                 ro_sort.ensure((size_t)E * s.acap);
@@ -1288,13 +1282,11 @@ public:
                     const size_t par_stride = ((size_t)E + (size_t)kXcds * kMaxSplit) * n_groups() * slots;
                     ro_items.ensure(2 * par_stride);
                     ro_cnt.ensure(2 * kXcds * kObsCntPad * kMaxSplit);
-                    const char* xv = getenv("MFX_ITEM_XCD");        // A/B only: 0 = one shared list
-                    ra.obs_lists = xv && atoi(xv) == 0 ? 1 : kXcds;
+                    ra.obs_lists = kXcds;                           // one list per XCD (profiles/r02_xcd_items_ab.txt)
                     ra.obs_items = ro_items.p; ra.obs_cnt = ro_cnt.p;
                     ra.obs_par_stride = par_stride; ra.obs_item_rows = R;
                     MFX_HIP_THROW(observe_items_grid(gp, R, &ro_item_grid));
-                    const char* gd = getenv("MFX_ITEM_GRID_DIV");   // sweeps only
-                    ro_item_grid = std::max(1, ro_item_grid / (gd ? std::max(1, atoi(gd)) : kItemGridDiv));
+                    ro_item_grid = std::max(1, ro_item_grid / kItemGridDiv);
                     if (ro_item_grid >= kXcds) ro_item_grid -= ro_item_grid % kXcds;   // as many per XCD
                     // the queue-driven kernel: item words hold 13 env bits and 6 chunk bits
                     const char* rv = getenv("MFX_BIGQ_ROWS");                  // sweeps only
@@ -1349,11 +1341,8 @@ public:
                         ra.q_si = ro_q_si.p; ra.q_done = ro_q_done.p; ra.q_list_cap = lcap;
                         ra.obs_item_rows = Rq;
                         if (ra.few_pipe) {
-                            const char* fw = getenv("MFX_FEW_WAVE_MAX");        // A/B only
                             // (at most 64: attack_wave / move_wave give each attacker and mover one lane)
-                            ra.few_wave_max = fw ? std::min(std::max(0, atoi(fw)), kFewWaveMax) : kFewWaveMax;
-                            const char* fo = getenv("MFX_FEW_OVERLAP");         // A/B only: 0 = file, then step
-                            ra.few_overlap = !(fo && atoi(fo) == 0);
+                            ra.few_wave_max = kFewWaveMax;
                             ra.few_snap_bytes = few_snap_bytes(s.cells_n, s.cap, n_groups());
                             ro_snap.ensure((size_t)E * 2 * ra.few_snap_bytes);
                             ro_q_step.ensure(kXcds);
@@ -1392,10 +1381,8 @@ public:
                 const char* pv = getenv("MFX_ROLLOUT_PIPE");
                 ro_pipe = pv ? atoi(pv) != 0 : kPipeDefault;
                 if (ro_pipe) {
-                    const char* a = getenv("MFX_PIPE_STEP_PER_CU");
-                    const char* b = getenv("MFX_PIPE_OBS_PER_CU");
-                    MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, 1, a ? atoi(a) : kPipeStepPerCu, &ro_grid));
-                    MFX_HIP_THROW(rollout_obs_grid(gp, s, ra.rowcap, b ? atoi(b) : kPipeObsPerCu, &ro_obs_grid));
+                    MFX_HIP_THROW(rollout_grid(gp, s, ra.rowcap, 1, kPipeStepPerCu, &ro_grid));
+                    MFX_HIP_THROW(rollout_obs_grid(gp, s, ra.rowcap, kPipeObsPerCu, &ro_obs_grid));
                     alloc_twin();
                     ro_par = 0;
                     ro_pipe_host[0].s = s; ro_pipe_host[0].ra = ra; ro_pipe_host[0].w = twin_state();

@@ -230,11 +230,6 @@ struct RolloutArgs {
     int renumber;                   // large envs: clear_dead renumbers the slots to the list order, so
                                     //   the per-slot arrays of the live agents stay dense (rid keeps ids);
                                     //   2: without the identity fast path (A/B only)
-    int queue_tiers;                // k_rollout: each workgroup's two initial envs come from two tiers of the
-                                    //   heaviest-first order (ranks b, 2G - 1 - b of G workgroups), it claims one
-                                    //   env ahead instead of two, and files envs by their weight over the next
-                                    //   launch (a cap restart inside it counts) -- 0: round 3 (A/B only), 2: tiers
-                                    //   without the restart-aware weights (A/B only)
     int lds_step;                   // few LDS-sized envs on the queue kernel: big_env_step stages the env in
                                     //   LDS for the step and writes it back (BigLayout::img)
     float* obs_mm;                  // large envs (k_rollout_big): [E][G][VH*VW] minimap density and
@@ -258,7 +253,6 @@ struct RolloutArgs {
     size_t q_list_cap;              //   items per list and parity
     int few_pipe;                   // few LDS-sized envs on the queue kernel, pipelined: one stepper workgroup
     int few_wave_max;               // few_pipe: the stepper's wave team (wave 0 alone) up to this many agents, else the workgroup
-    int few_overlap;                // few_pipe: wave 0 steps while the other waves drain the snapshot and file its items
                                     //   per env keeps it in LDS for the whole launch and steps it while the
                                     //   item workers observe the state the step started from, out of a
                                     //   per-env snapshot (few_snap, 2 parities) -- k_rollout_bigq<true>

@@ -79,7 +79,6 @@ extern "C" __attribute__((visibility("default"))) int mfx_store_ceiling(void* d_
         return mfx::fail("store_ceiling: bad arguments (buffer %p, region %zu B, shape %d)", d_buf, region_bytes, shape);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int form = shape >> 1;
-    const bool nt = shape & 1;
     const size_t chunk = form == 1 ? 8192 : form == 2 ? 16384 : 4096;
     const size_t region_chunks = region_bytes / chunk;
     const int grid_p = mfx::device_cus() * 8;

@@ -28,7 +28,6 @@ struct IsingEngine {
     DevBuf<uint32_t> mask;
     DevBuf<int32_t> nup_t;
     DevBuf<int32_t> err;
-    DevBuf<unsigned long long> scan_stats;   // MFX_ISING_SCAN_STATS diagnostics
     // mfx_ising_mfq_run_stream's two pass slots: pass p's words are generated and walked (gen stream) into slot
     // p % 2 while pass p - 1's episode runs out of the other (stream)
     struct Slot {
@@ -209,27 +208,14 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
             if (!sl.produced) MFX_HIP_THROW(hipEventCreateWithFlags(&sl.produced, hipEventDisableTiming));
             if (!sl.consumed) MFX_HIP_THROW(hipEventCreateWithFlags(&sl.consumed, hipEventDisableTiming));
         }
-        if (!e->gen) {
-            const char* gp = getenv("MFX_ISING_GEN_PRIO");           // A/B only: the gen stream's priority
-            if (gp) MFX_HIP_THROW(hipStreamCreateWithPriority(&e->gen, hipStreamNonBlocking, atoi(gp)));
-            else MFX_HIP_THROW(hipStreamCreateWithFlags(&e->gen, hipStreamNonBlocking));
-        }
+        if (!e->gen) MFX_HIP_THROW(hipStreamCreateWithFlags(&e->gen, hipStreamNonBlocking));
         e->err.ensure(1);
         e->spins_out.ensure((size_t)R * N);
     } catch (const std::exception& ex) {
         return mfx::fail("%s", ex.what());
     }
     MFX_HIP(hipMemsetAsync(e->err.p, 0, sizeof(int32_t), e->stream));
-    const char* ss = getenv("MFX_ISING_SCAN_STATS");                // diagnostics only
-    const bool want_stats = ss && atoi(ss) != 0;
-    if (want_stats) {
-        try { e->scan_stats.ensure(4); } catch (const std::exception& ex) { return mfx::fail("%s", ex.what()); }
-        MFX_HIP(hipMemsetAsync(e->scan_stats.p, 0, 4 * sizeof(unsigned long long), e->stream));
-    }
-    const char* rb = getenv("MFX_ISING_SCAN_RING");                  // A/B only: 16 / 24 / 32 blocks
-    const int ring = rb ? atoi(rb) : 24;                             // (24: 3.41e10 vs 3.32e10 with 32, 16384 replicas)
-    const char* ov = getenv("MFX_ISING_OVERLAP");                    // A/B only: 0 = one stream
-    hipStream_t gs = ov && atoi(ov) == 0 ? e->stream : e->gen;
+    hipStream_t gs = e->gen;                                         // the generation's own stream
     {   // the gen stream starts after the error word is cleared
         hipEvent_t ready = e->slot[0].consumed;
         MFX_HIP(hipEventRecord(ready, e->stream));
@@ -245,8 +231,6 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
         sa.mask = n_upd < N ? sl.mask.p : nullptr;
         sa.perm = n_upd < N ? sl.perm.p : nullptr;
         sa.err = e->err.p;
-        sa.stats = want_stats ? e->scan_stats.p : nullptr;
-        sa.ring = ring;
         return mfx::launch_ising_scan(sa, nr, st);
     };
     // pass p's generation and first walk (gen stream), into slot p % 2 once pass p - 2 has released it
@@ -293,13 +277,6 @@ MFX_API int mfx_ising_mfq_run_stream(void* h, int T, double temperature, double 
     int32_t err = 0;
     MFX_HIP(hipMemcpyAsync(&err, e->err.p, sizeof(err), hipMemcpyDeviceToHost, e->stream));
     MFX_HIP(hipStreamSynchronize(e->stream));
-    if (want_stats) {
-        unsigned long long st[4] = {};
-        MFX_HIP(hipMemcpy(st, e->scan_stats.p, sizeof(st), hipMemcpyDeviceToHost));
-        fprintf(stderr, "ising scan: %llu chunks, %.3f passes per chunk, %.2f words per chunk, %llu wave-reads past "
-                        "the window\n", st[0], st[0] ? (double)st[1] / st[0] : 0.0, st[0] ? (double)st[3] / st[0] : 0.0,
-                st[2]);
-    }
     if (err) return mfx::fail("ising mfq stream: a replica's draws ran past its %zu generated words", W);
     return 0;
 }

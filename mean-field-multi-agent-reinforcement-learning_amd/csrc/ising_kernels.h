@@ -43,9 +43,6 @@ struct IsingScanArgs {
     uint32_t* mask;                // [R][T][ceil(N / 32)] act_group bits (n_upd < N), else null
     uint16_t* perm;                // [R][N] scratch (n_upd < N)
     int32_t* err;                  // set to 1 when a replica's walk runs past wstride
-    int ring;                      // the LDS ring's blocks of 64 words: 16, 24 (the engine's default) or 32
-    unsigned long long* stats;     // diagnostics (MFX_ISING_SCAN_STATS): [0] chunks, [1] fixed-point passes,
-                                   // [2] words read past the ring's window, [3] words walked (null: none)
 };
 hipError_t launch_ising_scan(const IsingScanArgs& a, int R, hipStream_t st);
 

@@ -99,171 +99,10 @@ __device__ __forceinline__ int conv1_koff(int k) {
     return (ky * kQVW + kx) * kQNC + ci;
 }
 
-// rows: view row of compact agent i (null: i); view_ld: floats per view row.  out: [n][2,592].
-// d_n: the row count on the device (null: n); n is then this pass's upper bound and n_off the pass's first row.
-__global__ void __launch_bounds__(256, 1) k_qnet_conv(QNetDev p, const float* __restrict__ view, size_t view_ld,
-                                                      const int32_t* __restrict__ rows, int n, float* __restrict__ out,
-                                                      const int32_t* __restrict__ d_n, int n_off) {
-    extern __shared__ __attribute__((aligned(16))) float qsm[];
-    if (d_n) n = min(max(*d_n - n_off, 0), n);
-    if (n <= 0) return;
-    float* w1 = qsm;
-    float* w2 = w1 + kQK1 * kQCh;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 4, c = lane & 15;
-    float* vs = w2 + kQCh * kQW2tLd + wid * (kQViewLds + kQC1Lds);
-    float* c1 = vs + kQViewLds;
-    for (int i = threadIdx.x; i < kQK1 * kQCh; i += blockDim.x) w1[i] = p.w1[i];
-    for (int i = threadIdx.x; i < kQK2 * kQCh; i += blockDim.x) w2[(i % kQCh) * kQW2tLd + i / kQCh] = p.w2[i];
-    __syncthreads();
-    // conv1's B operands for all 16 k-steps stay in registers, so do the lane's im2col offsets
-    float b1r[16][2];
-    int koff[16];
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-        b1r[kk][0] = w1[(kk * 4 + h) * kQCh + c];
-        b1r[kk][1] = w1[(kk * 4 + h) * kQCh + 16 + c];
-        koff[kk] = conv1_koff(kk * 4 + h);
-    }
-    const float bias1a = p.b1[c], bias1b = p.b1[16 + c], bias2a = p.b2[c], bias2b = p.b2[16 + c];
-    // the next agent's view is in flight in registers while this one is computed (19 floats per lane)
-    constexpr int kVR = (kQViewF + 63) / 64;
-    float vr[kVR];
-    auto fetch = [&](int i) {
-        if (i >= n) return;
-        const float* src = view + (size_t)(rows ? rows[i] : i) * view_ld;
-#pragma unroll
-        for (int j = 0; j < kVR; ++j) {
-            const int q = lane + j * 64;
-            vr[j] = q < kQViewF ? src[q] : 0.f;
-        }
-    };
-    const int step = gridDim.x * kQConvWaves;
-    fetch(blockIdx.x * kQConvWaves + wid);
-    for (int i = blockIdx.x * kQConvWaves + wid; i < n; i += step) {
-#pragma unroll
-        for (int j = 0; j < kVR; ++j) {
-            const int q = lane + j * 64;
-            if (q < kQViewF) vs[q] = vr[j];
-        }
-        qwave_sync();
-        fetch(i + step);
-        // ---- Conv1: 8 position tiles (121 of 128 rows) x 2 channel tiles, K 64
-        for (int mt = 0; mt < 8; ++mt) {
-            const int pa = min(mt * 16 + c, kQC1 * kQC1 - 1);
-            const int vb = ((pa / kQC1) * kQVW + pa % kQC1) * kQNC;
-            f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk) {
-                const float a = vs[vb + koff[kk]];
-                d0 = mfma4(a, b1r[kk][0], d0);
-                d1 = mfma4(a, b1r[kk][1], d1);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int pos = mt * 16 + h * 4 + r;
-                if (pos < kQC1 * kQC1) {
-                    c1[pos * kQC1Ld + c] = fmaxf(d0[r] + bias1a, 0.f);
-                    c1[pos * kQC1Ld + 16 + c] = fmaxf(d1[r] + bias1b, 0.f);
-                }
-            }
-        }
-        qwave_sync();
-        // ---- Conv2: 5 position tiles (positions 0-79) x 2 channel tiles on the MFMA, K 288 = 9 (ky, kx) blocks x
-        // 32 ci, and position 80 -- the 81st, which a sixth tile would carry with 15 rows of padding (16 % more MFMA
-        // work) -- on the VALU below.  Inside block b the 8 k-steps j give lane group h the channels ci = 8 h + j
-        // (any order of k is the same sum up to rounding), so a lane's A operands of a block (per tile) and B
-        // operands (per channel tile) are 8 consecutive floats: 14 ds_read_b128 per block for 80 MFMAs, the next
-        // block's in flight meanwhile.
-        constexpr int kMT2 = 5;
-        f32x4 acc[kMT2][2];
-        int cb[kMT2];
-#pragma unroll
-        for (int mt = 0; mt < kMT2; ++mt) {
-            const int pa = mt * 16 + c;
-            cb[mt] = ((pa / kQC2) * kQC1 + pa % kQC2) * kQC1Ld + 8 * h;
-            acc[mt][0] = {0.f, 0.f, 0.f, 0.f};
-            acc[mt][1] = {0.f, 0.f, 0.f, 0.f};
-        }
-        typedef float f32x8 __attribute__((ext_vector_type(8)));
-        // Each block's 14 reads go out in two parts under the previous block's MFMAs (9 before its first half,
-        // 5 before its second), so no wait ever has to name more than 15 newer LDS operations (lgkmcnt's range).
-        f32x8 p0[kMT2], q0[2], p1[kMT2], q1[2];
-        auto conv2_part = [&](int b, f32x8* a, f32x8* w, int part) {
-            const int ky = b / 3, kx = b % 3;
-            const int so = (ky * kQC1 + kx) * kQC1Ld;
-            if (part == 0) {
-#pragma unroll
-                for (int q = 0; q < 2; ++q) w[q] = *reinterpret_cast<const f32x8*>(w2 + (16 * q + c) * kQW2tLd + b * 32 + 8 * h);
-#pragma unroll
-                for (int mt = 0; mt < 3; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
-            } else {
-#pragma unroll
-                for (int mt = 3; mt < kMT2; ++mt) a[mt] = *reinterpret_cast<const f32x8*>(c1 + cb[mt] + so);
-            }
-        };
-        auto conv2_half = [&](const f32x8* a, const f32x8* w, int j0) {
-#pragma unroll
-            for (int j = j0; j < j0 + 4; ++j)
-#pragma unroll
-                for (int mt = 0; mt < kMT2; ++mt) {
-                    acc[mt][0] = mfma4(a[mt][j], w[0][j], acc[mt][0]);
-                    acc[mt][1] = mfma4(a[mt][j], w[1][j], acc[mt][1]);
-                }
-        };
-        // one block's MFMAs with the next block's reads interleaved (nb < 0: none)
-        auto conv2_step = [&](const f32x8* a, const f32x8* w, f32x8* na, f32x8* nw, int nb) {
-            if (nb >= 0) conv2_part(nb, na, nw, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            conv2_half(a, w, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (nb >= 0) conv2_part(nb, na, nw, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            conv2_half(a, w, 4);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        conv2_part(0, p0, q0, 0);
-        conv2_part(0, p0, q0, 1);
-#pragma unroll 1
-        for (int b = 0; b < 8; b += 2) {                 // ping-pong: block b in (p0, q0), b + 1 in (p1, q1)
-            conv2_step(p0, q0, p1, q1, b + 1);
-            conv2_step(p1, q1, p0, q0, b + 2);
-        }
-        conv2_step(p0, q0, p1, q1, -1);                  // block 8
-        float* o = out + (size_t)i * kQFlat;
-#pragma unroll
-        for (int mt = 0; mt < kMT2; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int pos = mt * 16 + h * 4 + r;
-                o[pos * kQCh + c] = fmaxf(acc[mt][0][r] + bias2a, 0.f);
-                o[pos * kQCh + 16 + c] = fmaxf(acc[mt][1][r] + bias2b, 0.f);
-            }
-        {
-            // position 80 (row 8, column 8) on the VALU: lane l sums output channel l % 32 over half l / 32 of
-            // the 288 k (blocks 0-3 and half of 4 / the rest), 16-B reads of the patch (broadcast) and of w2t
-            const int co = lane & 31, k0 = (lane >> 5) * 144;
-            const float4* wr = reinterpret_cast<const float4*>(w2 + co * kQW2tLd + k0);
-            float sum = 0.f;
-#pragma unroll 4
-            for (int q = 0; q < 36; ++q) {
-                const int k = k0 + 4 * q, b = k >> 5, ci = k & 31;
-                const float4 x = *reinterpret_cast<const float4*>(c1 + ((8 + b / 3) * kQC1 + 8 + b % 3) * kQC1Ld + ci);
-                const float4 w = wr[q];
-                sum = __builtin_fmaf(x.x, w.x, sum);
-                sum = __builtin_fmaf(x.y, w.y, sum);
-                sum = __builtin_fmaf(x.z, w.z, sum);
-                sum = __builtin_fmaf(x.w, w.w, sum);
-            }
-            sum += __shfl_xor(sum, 32);
-            if (lane < 32) o[80 * kQCh + co] = fmaxf(sum + p.b2[co], 0.f);
-        }
-        qwave_sync();                                    // vs / c1 are rewritten by the next agent
-    }
-}
-
-// The same forward with TWO waves per agent (8-wave workgroups, 4 agents per pass, one workgroup per CU): the pair
-// shares its agent's staged view and conv1 output in LDS -- so the 134 KB above hold 4 agents for 8 waves, two per
-// SIMD, where k_qnet_conv runs one -- and splits the work: conv1's position tiles 0-3 / 4-7, conv2's output channels
+// Conv1 + Conv2 (implicit GEMMs from LDS) with TWO waves per agent (8-wave workgroups, 4 agents per pass, one
+// workgroup per CU): the pair shares its agent's staged view and conv1 output in LDS -- so the 134 KB above hold 4
+// agents for 8 waves, two per SIMD (round 5; the round-3/4 one-wave-per-agent k_qnet_conv ran one) -- and splits the
+// work: conv1's position tiles 0-3 / 4-7, conv2's output channels
 // 0-15 / 16-31 (5 position tiles each, its position 80 on the VALU), the view's 64-float chunks even / odd.  Two
 // workgroup barriers per pass: after the view is staged, after conv1.  <= 256 VGPRs (launch bounds 512, 1).
 constexpr int kQConv2Agents = 4;
@@ -422,8 +261,8 @@ __global__ void __launch_bounds__(512, 1) k_qnet_conv2(QNetDev p, const float* _
 // ------------------------------------------------------------------------------------------ head
 
 // kImg (the default): Dense-Obs over its weight image (wg_gemm_i, direct-to-LDS chunks) with the conv activations
-// through an LDS ring filled two chunks ahead, its accumulators starting at the bias; else the register-staged
-// wg_gemm_t (A/B: MFX_QNET_IMG=0).  LDS: the image path's 32 KB of chunks + the 12 KB ring, then the small layers'
+// through an LDS ring filled two chunks ahead, its accumulators starting at the bias; else (no weights set yet) the
+// register-staged wg_gemm_t.  LDS: the image path's 32 KB of chunks + the 12 KB ring, then the small layers'
 // wg_gemm_t staging from offset 0.
 constexpr size_t kQHeadImgSmem = kImgSmem + 3 * 1024 * 4 > kQHeadSmem ? kImgSmem + 3 * 1024 * 4 : kQHeadSmem;
 template <typename PT, bool kImg>
@@ -713,18 +552,11 @@ static int qnet_run(QNetHandle* q, const float* view, size_t view_ld, const floa
                                            : (const void*)(static_cast<const float*>(prob) + (size_t)off * prob_ld);
         float* qo = q_out ? q_out + (size_t)off * q->dev.A : nullptr;
         int32_t* ao = act ? (r.rows ? act : act + off) : nullptr;
-        static const bool conv_pair = [] { const char* e = getenv("MFX_QNET_CONV"); return !(e && atoi(e) == 1); }();
-        if (conv_pair) {                 // (A/B: MFX_QNET_CONV=1 runs the one-wave-per-agent k_qnet_conv)
-            const int cgrid = std::min((m + kQConv2Agents - 1) / kQConv2Agents, cus);
-            k_qnet_conv2<<<cgrid, 512, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p, d_n, off);
-        } else {
-            const int cgrid = std::min((m + kQConvWaves - 1) / kQConvWaves, cus * 8);
-            k_qnet_conv<<<cgrid, 256, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p, d_n, off);
-        }
+        const int cgrid = std::min((m + kQConv2Agents - 1) / kQConv2Agents, cus);
+        k_qnet_conv2<<<cgrid, 512, kQConvSmem, st>>>(q->dev, v, view_ld, r.rows, m, q->conv.p, d_n, off);
         MFX_HIP(hipGetLastError());
         const int hgrid = (m + 16 * kQHeadWaves - 1) / (16 * kQHeadWaves);
-        const char* iv = getenv("MFX_QNET_IMG");                   // A/B only: 0 = wg_gemm_t's register staging
-        const bool img = q->imaged && !(iv && atoi(iv) == 0);
+        const bool img = q->imaged;
 #define MFX_QHEAD(PT, IMG)                                                                                         \
         k_qnet_head<PT, IMG><<<hgrid, 256, IMG ? kQHeadImgSmem : kQHeadSmem, st>>>(                                  \
             q->dev, q->conv.p, m, f, feat_ld, static_cast<const PT*>(pb), prob_ld, r, qo, ao, d_n, off)

@@ -17,6 +17,9 @@
 namespace mfx {
 
 constexpr int kRowCols = 8;
+#ifndef MFX_ROWS_PER_CU
+#define MFX_ROWS_PER_CU 2            // k_rows_pipe workgroups per CU (A/B builds: make variant VFLAGS=-DMFX_ROWS_PER_CU=n)
+#endif
 constexpr int64_t kBigRow = 512;          // columns at least this wide get a per-column vector loop
 
 struct RowCols {
@@ -131,16 +134,21 @@ __global__ void __launch_bounds__(256) k_rows_copy(RowCols c, const int64_t* __r
 }
 
 // The same move, software-pipelined, for the common shape (MemoryGroup.sample, tight, push: at most one wide
-// column, 4-B aligned, <= 64 x kPipeU dwords per row, and at most 64 narrow units): each wave keeps two rows in
+// column, 4-B aligned, <= 64 x 4 kPipeQ + 3 dwords per row, and at most 64 narrow units): each wave keeps two rows in
 // flight -- row k + 1's loads are issued before row k's stores, so the in-order vmcnt of gfx9 lets the stores
 // of one row drain under the loads of the next instead of serialising load -> store per row -- and reads its row
 // indices through scalar loads (the row is wave-uniform), which wait on lgkmcnt, not behind the data loads.
-constexpr int kPipeU = 20;
+// The wide column moves in 16-B units at its rows' 4-B alignment (global_load / store_dwordx4 need only dword
+// alignment on gfx950: one 1-KiB wave-instruction per 1 KiB of row, where dword units took four 256-B ones; +1.5 %,
+// profiles/r06_replay_ab.txt), its last wdw % 4 dwords by single lanes.
+constexpr int kPipeQ = 5;
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 struct PipeRow {
     int64_t s, d;
     bool ok;
     uint32_t u;                    // this lane's narrow unit (dword, or byte in the low 8 bits)
-    uint32_t v[kPipeU];            // this lane's dwords of the wide column
+    u32x4a4 q[kPipeQ];             // this lane's 16-B units of the wide column
+    uint32_t t;                    // this lane's tail dword
 };
 
 __global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wdw, const int64_t* __restrict__ idx,
@@ -181,11 +189,13 @@ __global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wd
         }
         if (wk >= 0) {
             const uint32_t* sp = reinterpret_cast<const uint32_t*>(c.src[wk] + r.s * c.bytes[wk]);
+            const int64_t nq = wdw >> 2;
 #pragma unroll
-            for (int j = 0; j < kPipeU; ++j) {
+            for (int j = 0; j < kPipeQ; ++j) {
                 const int64_t q = lane + 64 * j;
-                if (q < wdw) r.v[j] = sp[q];
+                if (q < nq) r.q[j] = reinterpret_cast<const u32x4a4*>(sp)[q];
             }
+            if (lane < (wdw & 3)) r.t = sp[4 * nq + lane];
         }
     };
     auto put = [&](const PipeRow& r) {
@@ -197,11 +207,13 @@ __global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wd
         }
         if (wk >= 0) {
             uint32_t* dp = reinterpret_cast<uint32_t*>(c.dst[wk] + r.d * c.bytes[wk]);
+            const int64_t nq = wdw >> 2;
 #pragma unroll
-            for (int j = 0; j < kPipeU; ++j) {
+            for (int j = 0; j < kPipeQ; ++j) {
                 const int64_t q = lane + 64 * j;
-                if (q < wdw) dp[q] = r.v[j];
+                if (q < nq) reinterpret_cast<u32x4a4*>(dp)[q] = r.q[j];
             }
+            if (lane < (wdw & 3)) dp[4 * nq + lane] = r.t;
         }
     };
     PipeRow a, b;
@@ -219,81 +231,6 @@ __global__ void __launch_bounds__(256) k_rows_pipe(RowCols c, int wk, int64_t wd
         fetch(a);
         put(b);
         i = i2;
-    }
-}
-
-// A/B form (MFX_ROWS_PIPE=2/3): R rows per wave loaded together, then stored together (R x ~4.7 KB in flight per
-// wave instead of two rows staggered); kNt: the destination rows written with nontemporal stores.
-template <int R, bool kNt>
-__global__ void __launch_bounds__(256) k_rows_batch(RowCols c, int wk, int64_t wdw, const int64_t* __restrict__ idx,
-                                                    int64_t src_mod, int64_t src_rows, int64_t dst_start,
-                                                    int64_t dst_cap, int64_t n) {
-    const int lane = threadIdx.x & 63;
-    const int64_t W = (int64_t)gridDim.x * 4;
-    const int64_t first = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    const int units = c.ustart[kRowCols];
-    int uk = -1, uoff = 0, uw = 0;
-    if (lane < units) {
-        uk = 0;
-        while (lane >= c.ustart[uk + 1]) ++uk;
-        uw = c.ubytes[uk];
-        uoff = (lane - c.ustart[uk]) * uw;
-    }
-    for (int64_t i0 = first; i0 < n; i0 += (int64_t)R * W) {
-        PipeRow r[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int64_t i = i0 + k * W;
-            r[k].ok = i < n;
-            if (!r[k].ok) continue;
-            const int64_t raw = idx ? idx[i] : i;
-            const int64_t sidx = rows_src(raw, src_mod, src_rows);
-            if (sidx < 0) {
-                if (lane == 0) rows_bad(raw);
-                r[k].ok = false;
-                continue;
-            }
-            int64_t d = dst_start + i;
-            if (dst_cap > 0 && d >= dst_cap) d %= dst_cap;
-            r[k].s = sidx;
-            r[k].d = d;
-        }
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            if (!r[k].ok) continue;
-            if (uk >= 0) {
-                const char* sp = c.src[uk] + r[k].s * c.bytes[uk] + uoff;
-                r[k].u = uw == 4 ? *reinterpret_cast<const uint32_t*>(sp) : (uint32_t)*reinterpret_cast<const uint8_t*>(sp);
-            }
-            if (wk >= 0) {
-                const uint32_t* sp = reinterpret_cast<const uint32_t*>(c.src[wk] + r[k].s * c.bytes[wk]);
-#pragma unroll
-                for (int j = 0; j < kPipeU; ++j) {
-                    const int64_t q = lane + 64 * j;
-                    if (q < wdw) r[k].v[j] = sp[q];
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            if (!r[k].ok) continue;
-            if (uk >= 0) {
-                char* dp = c.dst[uk] + r[k].d * c.bytes[uk] + uoff;
-                if (uw == 4) *reinterpret_cast<uint32_t*>(dp) = r[k].u;
-                else *reinterpret_cast<uint8_t*>(dp) = (uint8_t)r[k].u;
-            }
-            if (wk >= 0) {
-                uint32_t* dp = reinterpret_cast<uint32_t*>(c.dst[wk] + r[k].d * c.bytes[wk]);
-#pragma unroll
-                for (int j = 0; j < kPipeU; ++j) {
-                    const int64_t q = lane + 64 * j;
-                    if (q < wdw) {
-                        if (kNt) __builtin_nontemporal_store(r[k].v[j], dp + q);
-                        else dp[q] = r[k].v[j];
-                    }
-                }
-            }
-        }
     }
 }
 
@@ -338,14 +275,14 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
         }
     }
     for (int k = n_cols; k <= kRowCols; ++k) c.ustart[k] = units;
-    // the pipelined form takes at most one wide column (4-B aligned, <= 64 x kPipeU dwords) and <= 64 units
+    // the pipelined form takes at most one wide column (4-B aligned, <= 64 x 4 kPipeQ + 3 dwords) and <= 64 units
     int wide = -1, n_wide = 0;
     for (int k = 0; k < n_cols; ++k)
         if (!c.ubytes[k]) { wide = k; ++n_wide; }
     const bool pipe = n_wide <= 1 && units <= 64 &&
                       (wide < 0 || ((((uintptr_t)dst[wide] | (uintptr_t)src[wide] | (uintptr_t)row_bytes[wide]) & 3) == 0 &&
-                                    row_bytes[wide] / 4 <= 64 * kPipeU));
-    const char* pe = getenv("MFX_ROWS_PIPE");              // 0: the one-row-per-wave form (A/B, tests)
+                                    row_bytes[wide] / 4 <= 64 * 4 * kPipeQ + 3));
+    const char* pe = getenv("MFX_ROWS_PIPE");              // 0: the one-row-per-wave form (tests)
     const int use_pipe = pe ? atoi(pe) : 1;
     const int64_t wgs = (n + 3) / 4;
     if (pipe && use_pipe) {
@@ -356,20 +293,14 @@ MFX_API int mfx_rows_copy(int n_cols, void* const* dst, const void* const* src, 
                 hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
             return n_cu;
         }();
-        // 4 workgroups per CU: 0.555-0.559 of the HBM peak on the MF-Q sample against 0.464 / 0.520 at 7 / 14 and
-        // 0.510-0.537 for the one-row-per-wave form (profiles/r04_replay_ab.txt)
-        static const int per_cu = [] { const char* e = getenv("MFX_ROWS_WG_PER_CU"); return e ? atoi(e) : 4; }();
-        const int64_t cap = (int64_t)cus * per_cu;
+        // 2 workgroups per CU with the 16-B units: 0.573-0.577 of the HBM peak on the MF-Q sample against 0.565 at 4
+        // and 0.49 at 8 (profiles/r06_replay_ab.txt; round 4 with dword units: 0.555-0.559 at 4, 0.464 / 0.520 at 7
+        // / 14, 0.510-0.537 for the one-row-per-wave form; four rows loaded then stored, and nontemporal stores, lost:
+        // profiles/r04_replay_ab.txt)
+        const int64_t cap = (int64_t)cus * MFX_ROWS_PER_CU;
         const int grid = (int)(wgs < cap ? wgs : cap);
         const int64_t wdw = wide >= 0 ? row_bytes[wide] / 4 : 0;
-        const char* ne = getenv("MFX_ROWS_NT");
-        const bool nt = ne && atoi(ne) == 1;
-        hipStream_t st = (hipStream_t)stream;
-        if (use_pipe == 2 && nt) k_rows_batch<4, true><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
-        else if (use_pipe == 2) k_rows_batch<4, false><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
-        else if (use_pipe == 3 && nt) k_rows_batch<2, true><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
-        else if (use_pipe == 3) k_rows_batch<2, false><<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
-        else k_rows_pipe<<<grid, 256, 0, st>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
+        k_rows_pipe<<<grid, 256, 0, (hipStream_t)stream>>>(c, wide, wdw, d_idx, src_mod, src_rows, dst_start, dst_cap, n);
         MFX_HIP(hipGetLastError());
         return 0;
     }

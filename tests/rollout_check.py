@@ -207,15 +207,16 @@ def device_records(eng, envs):
         eng.rollout_copy_at("episode_return", out["ep_return"][j], e * G * 4)
         eng.rollout_copy_at("group_num", out["group_num"][j], e * G * 4)
     getters = {"ids": (GET_ID, torch.int32, 1), "pos": (GET_POS, torch.int32, 2), "hp": (GET_HP, torch.float32, 1)}
-    dev = {}
-    idx = torch.tensor(envs, dtype=torch.int64, device="cuda")
+    full = {}
     for name, (what, dt, w) in getters.items():
-        dev[name] = []
+        full[name] = []
         for g in range(G):
             buf = torch.empty((E, rc, w), dtype=dt, device="cuda")
-            eng.get(g, what, buf, rc)
-            dev[name].append(buf.index_select(0, idx))
-    eng.sync()
+            eng.get(g, what, buf, rc)                  # (on the engine's stream)
+            full[name].append(buf)
+    eng.sync()                                         # before torch reads them on its own stream
+    idx = torch.tensor(envs, dtype=torch.int64, device="cuda")
+    dev = {name: [b.index_select(0, idx) for b in bufs] for name, bufs in full.items()}
     rec = {key: ([x.numpy() for x in v] if isinstance(v, list) else v.numpy()) for key, v in out.items()}
     for name in getters:
         rec[name] = [x.cpu().numpy() for x in dev[name]]

@@ -86,15 +86,16 @@ def _random_scenario(lib_path, map_size, n0, n1, seed, steps, n_walls, episodes=
     return out
 
 
-@pytest.mark.parametrize("fast", ["1", "0"])
-@pytest.mark.parametrize("map_size,n0,n1,seed,walls", [
-    (12, 5, 9, 1, 6), (20, 30, 30, 2, 20), (33, 60, 40, 3, 50), (64, 128, 128, 4, 0), (110, 300, 250, 5, 100),
-    # envs too large for k_step's LDS copy: k_step_big (attack_big, band sort, move_jump) on random crowds
-    (180, 1500, 1500, 6, 300), (256, 2500, 2000, 7, 600)])
+_SCENARIOS = [(12, 5, 9, 1, 6), (20, 30, 30, 2, 20), (33, 60, 40, 3, 50), (64, 128, 128, 4, 0), (110, 300, 250, 5, 100)]
+# envs too large for k_step's LDS copy: k_step_big (attack_big, band sort, move_jump) on random crowds -- one run each:
+# these maps never take the drop-in's fast step, so MFX_DROPIN_FAST=0 would repeat the same path
+_LARGE = [(180, 1500, 1500, 6, 300), (256, 2500, 2000, 7, 600)]
+
+
+@pytest.mark.parametrize("map_size,n0,n1,seed,walls,fast",
+                         [s + (f,) for s in _SCENARIOS for f in ("1", "0")] + [s + ("1",) for s in _LARGE])
 def test_hip_matches_oracle_random_scenarios(map_size, n0, n1, seed, walls, fast, monkeypatch):
     monkeypatch.setenv("MFX_DROPIN_FAST", fast)
-    if fast == "0" and map_size > 110:
-        pytest.skip("the large maps never take the fast step")
     ref = _random_scenario(common.ORACLE_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
     got = _random_scenario(common.HIP_LIB, map_size, n0, n1, seed, 60, walls, episodes=2)
     assert len(got) == len(ref)
