@@ -242,12 +242,18 @@ int mfx_acnet_act_rollout(void *handle, const float *d_view, const float *d_feat
 /* ---------------------------------------------------------------- part 6: replay rows */
 /* The data path of the replay buffers (algo/tools.py:26-362): for i < n, row idx[i] (or i; modulo src_mod
  * when > 0) of every source column -> row dst_start + i (modulo dst_cap when > 0) of its destination column;
- * n_cols <= 8, row_bytes per column; one launch (csrc/replay_kernels.hip).  src_rows: rows of every source
+ * n_cols <= 12, row_bytes per column; one launch (csrc/replay_kernels.hip).  src_rows: rows of every source
  * column -- without src_mod an index in [-src_rows, 0) counts from the end, as numpy's indexing does; any other
  * index outside [0, src_rows) (the reference's numpy indexing raises IndexError) skips the row and is reported by
  * mfx_rows_copy_error (synchronising; -1 and *bad_index when one was met, -1 included, then cleared). */
 int mfx_rows_copy(int n_cols, void *const *dst, const void *const *src, const int64_t *row_bytes, const int64_t *d_idx,
                   int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap, int64_t n, void *stream);
+/* The same move with the columns whose bit is set in shift_mask reading source row idx[i] + shift (before the
+ * modulo, checked the same way): MemoryGroup.sample's next-state columns at next_idx = (idx + 1) % nb_entries
+ * (algo/tools.py:239-262) in the launch of the current-state columns.  mfx_rows_copy = shift_mask 0. */
+int mfx_rows_copy_shift(int n_cols, void *const *dst, const void *const *src, const int64_t *row_bytes,
+                        const int64_t *d_idx, int64_t src_mod, int64_t src_rows, int64_t dst_start, int64_t dst_cap,
+                        int64_t n, uint32_t shift_mask, int64_t shift, void *stream);
 int mfx_rows_copy_error(int64_t *bad_index, void *stream);
 
 /* ---------------------------------------------------------------- measurement */

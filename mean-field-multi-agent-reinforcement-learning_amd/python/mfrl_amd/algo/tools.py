@@ -41,22 +41,22 @@ def _dev(x, dtype, device="cuda"):
     return torch.as_tensor(np.asarray(x), dtype=dtype, device=device)
 
 
-def _move(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
-    """rows_copy on the device (one HIP launch for every column); torch indexing for device='cpu'."""
+def _move(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None, shift_mask=0, shift=0):
+    """rows_copy on the device (one HIP launch for every column); torch indexing for device='cpu'.  Columns k
+    with bit k of shift_mask set read row idx + shift."""
     if dst[0].is_cuda:
         assert all(d.is_contiguous() for d in dst)
-        replay.rows_copy(dst, [x.contiguous() for x in src], idx, src_mod, dst_start, dst_cap, n)
+        replay.rows_copy(dst, [x.contiguous() for x in src], idx, src_mod, dst_start, dst_cap, n, shift_mask, shift)
         return
     if n is None:
         n = len(idx) if idx is not None else len(src[0])
-    s = torch.arange(n) if idx is None else idx.to(torch.int64)
-    if src_mod:
-        s = s % src_mod
+    s0 = torch.arange(n) if idx is None else idx.to(torch.int64)
     d = torch.arange(n) + dst_start
     if dst_cap:
         d = d % dst_cap
-    for a, b in zip(dst, src):
-        a[d] = b[s]
+    for k, (a, b) in enumerate(zip(dst, src)):
+        s = s0 + shift if shift_mask >> k & 1 else s0
+        a[d] = b[s % src_mod if src_mod else s]
 
 
 def ring_append(bufs, srcs, idx=None):
@@ -238,22 +238,19 @@ class MemoryGroup:
 
     def sample(self):
         idx = np.random.choice(self.nb_entries, size=self.batch_size)
-        next_idx = (idx + 1) % self.nb_entries
         idx = torch.as_tensor(idx, device=self.device)
-        next_idx = torch.as_tensor(next_idx, device=self.device)
         B = len(idx)
         cur = [self.obs0, self.feat0, self.actions, self.rewards, self.terminals, self.masks]
         nxt = [self.obs0, self.feat0]
         if self.use_mean:
             cur.append(self.prob)
             nxt.append(self.prob)
-
-        def gather(bufs, ix):                   # one move for every column sampled at these indices
-            out = [torch.empty((B,) + tuple(b.data.shape[1:]), dtype=b.data.dtype, device=self.device) for b in bufs]
-            _move(out, [b.data for b in bufs], ix, src_mod=self.nb_entries)
-            return out
-
-        c, x = gather(cur, idx), gather(nxt, next_idx)
+        # one move for the current columns at idx and the next-state columns at the reference's next_idx =
+        # (idx + 1) % nb_entries (tools.py:241): the two rows of an entry are adjacent in the ring
+        out = [torch.empty((B,) + tuple(b.data.shape[1:]), dtype=b.data.dtype, device=self.device) for b in cur + nxt]
+        shift_mask = ((1 << len(nxt)) - 1) << len(cur)
+        _move(out, [b.data for b in cur + nxt], idx, src_mod=self.nb_entries, shift_mask=shift_mask, shift=1)
+        c, x = out[:len(cur)], out[len(cur):]
         obs, feature, actions, rewards, dones, masks = c[:6]
         obs_next, feature_next = x[:2]
         if self.use_mean:

@@ -8,16 +8,17 @@ import torch
 
 from . import check, lib
 
-_MAX_COLS = 8
+_MAX_COLS = 12
 
 
-def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
+def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None, shift_mask=0, shift=0):
     """For i < n: row (idx[i] if idx is not None else i), taken modulo src_mod if > 0, of every tensor in
     `src` -> row dst_start + i (modulo dst_cap if > 0) of the matching tensor in `dst`.  Tensors: CUDA,
     contiguous, first dimension = rows, equal row byte sizes pairwise.  Without src_mod, an index in
     [-rows, 0) counts from the end as numpy's does; any other index outside the source rows is skipped on the
     device and raised by the next check_errors() (the reference's numpy indexing raises IndexError at once;
-    checking here would synchronise every move)."""
+    checking here would synchronise every move).  Columns k with bit k of shift_mask set read row idx[i] + shift
+    instead (before the modulo): MemoryGroup.sample's next-state columns in the launch of the current ones."""
     assert len(dst) == len(src) and 0 < len(dst) <= _MAX_COLS
     if n is None:
         n = len(idx) if idx is not None else src[0].shape[0]
@@ -36,12 +37,14 @@ def rows_copy(dst, src, idx=None, src_mod=0, dst_start=0, dst_cap=0, n=None):
     L = lib()
     L.mfx_rows_copy.restype = ctypes.c_int
     P = ctypes.c_void_p * k
-    check(L.mfx_rows_copy(k, P(*[d.data_ptr() for d in dst]), P(*[s.data_ptr() for s in src]),
-                          (ctypes.c_int64 * k)(*rb), ctypes.c_void_p(idx.data_ptr() if idx is not None else 0),
-                          ctypes.c_int64(int(src_mod)), ctypes.c_int64(int(src_rows)), ctypes.c_int64(int(dst_start)),
-                          ctypes.c_int64(int(dst_cap)), ctypes.c_int64(int(n)),
-                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
-          "mfx_rows_copy")
+    L.mfx_rows_copy_shift.restype = ctypes.c_int
+    check(L.mfx_rows_copy_shift(k, P(*[d.data_ptr() for d in dst]), P(*[s.data_ptr() for s in src]),
+                                (ctypes.c_int64 * k)(*rb), ctypes.c_void_p(idx.data_ptr() if idx is not None else 0),
+                                ctypes.c_int64(int(src_mod)), ctypes.c_int64(int(src_rows)),
+                                ctypes.c_int64(int(dst_start)), ctypes.c_int64(int(dst_cap)), ctypes.c_int64(int(n)),
+                                ctypes.c_uint32(int(shift_mask)), ctypes.c_int64(int(shift)),
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+          "mfx_rows_copy_shift")
 
 
 def check_errors():

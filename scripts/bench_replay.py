@@ -1,7 +1,8 @@
 """Replay data path throughput: MemoryGroup.sample of the MF-Q learner
 (examples/battle_model/algo/tools.py:239-262 -> mfrl_amd.algo.tools.MemoryGroup.sample): every column of a
 minibatch gathered at random row indices (view, feature, action, reward, terminal, mask, mean action) and the
-next-state columns at idx + 1 -- two k_rows_copy launches (csrc/replay_kernels.hip).  Sampled rows per second
+next-state columns at idx + 1 -- one mfx_rows_copy_shift launch (csrc/replay_kernels.hip; --two-launches: the
+current and next-state columns as two launches, round 6's form).  Sampled rows per second
 over a large batch, the kernel's bytes (read + write of every row) against the HBM roofline, next to the
 reference's numpy fancy indexing (MetaBuffer.sample, tools.py:38-40) of the same columns on one host thread.
 
@@ -20,6 +21,7 @@ ap.add_argument("--capacity", type=int, default=1 << 18)
 ap.add_argument("--batch", type=int, default=1 << 16)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--cpu-seconds", type=float, default=10.0)
+ap.add_argument("--two-launches", action="store_true")
 a = ap.parse_args()
 
 import numpy as np  # noqa: E402
@@ -44,8 +46,12 @@ nidx = (idx + 1) % C
 
 
 def sample():
-    rows_copy(outs_c, [bufs[k] for k in cur], idx, src_mod=C)
-    rows_copy(outs_n, [bufs[k] for k in nxt], nidx, src_mod=C)
+    if a.two_launches:
+        rows_copy(outs_c, [bufs[k] for k in cur], idx, src_mod=C)
+        rows_copy(outs_n, [bufs[k] for k in nxt], nidx, src_mod=C)
+    else:
+        rows_copy(outs_c + outs_n, [bufs[k] for k in cur + nxt], idx, src_mod=C,
+                  shift_mask=((1 << len(nxt)) - 1) << len(cur), shift=1)
 
 
 for _ in range(3):
@@ -83,7 +89,8 @@ line = {"metric": "replay minibatch rows sampled/sec (MemoryGroup.sample, MF-Q c
         "wall_rows_per_s": B * a.reps / wall,
         "roofline": {"bound": "hbm", "achieved": bytes_per_row * B / (med * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
                      "frac": bytes_per_row * B / (med * 1e-3) / 1e9 / 8000.0, "bytes_per_unit": bytes_per_row,
-                     "kernel": "k_rows_copy x2 (current columns, next-state columns)"},
+                     "kernel": "k_rows_pipe x2 (current columns, next-state columns)" if a.two_launches else
+                     "k_rows_pipe (current + next-state columns, one launch)"},
         "cpu_baseline": {"value": rows / cdt, "unit": "rows/s", "cores": 1, "kind": "port",
                          "sample": "numpy fancy indexing of the same 7 + 3 columns, 4096-row draws from a %d-row host "
                                    "buffer for %.0f s (MetaBuffer.sample's self._data[idx])" % (Cc, a.cpu_seconds)}}

@@ -20,8 +20,8 @@ def _cols(n, gen):
 @pytest.mark.parametrize("n_src,n,cap,start,mod", [(1000, 1000, 0, 0, 0), (1000, 700, 2000, 1500, 0),
                                                    (300, 257, 300, 250, 300), (50, 1, 0, 7, 0), (40000, 33333, 0, 0, 0)])
 def test_rows_copy_matches_torch_indexing(n_src, n, cap, start, mod, pipe, monkeypatch):
-    """pipe 1: the two-rows-in-flight form (k_rows_pipe: one wide column, <= 64 narrow units -- these five columns);
-    0: the one-row-per-wave form (k_rows_copy, which also takes every other column shape)."""
+    """pipe 1: the two-rows-in-flight form (k_rows_pipe<1, 1>: one wide column, <= 64 narrow units -- these five
+    columns); 0: the one-row-per-wave form (k_rows_copy, which also takes every other column shape)."""
     monkeypatch.setenv("MFX_ROWS_PIPE", pipe)
     from mfrl_amd.replay import rows_copy
     gen = torch.Generator(device="cuda").manual_seed(n + start)
@@ -80,3 +80,36 @@ def test_rows_copy_out_of_range_index_raises():
     rows_copy(dst, src, torch.tensor([2, -100], dtype=torch.int64, device="cuda"), n=2)
     with pytest.raises(IndexError, match="index -100 out of range"):
         check_errors()
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("n_src,n,mod,n_next", [(4096, 3000, 4096, 2), (300, 257, 250, 2), (1000, 5, 1000, 1),
+                                                (2000, 1999, 2000, 3)])
+def test_rows_copy_shifted_columns(n_src, n, mod, n_next, pipe, monkeypatch):
+    """MemoryGroup.sample's fused move (mfx_rows_copy_shift): the current columns at idx and next-state copies of
+    the first n_next of them at (idx + 1) % mod, in one launch.  n_next 2: two wide columns + 90 narrow units (the
+    pipelined form's limits, k_rows_pipe<2, 2>); 1: k_rows_pipe<1, 1>; 3: three wide columns take k_rows_copy."""
+    monkeypatch.setenv("MFX_ROWS_PIPE", pipe)
+    from mfrl_amd.replay import check_errors, rows_copy
+    gen = torch.Generator(device="cuda").manual_seed(n + n_next)
+    src = _cols(n_src, gen)
+    nxt = [src[0], src[4], src[0]][:n_next]
+    cols = src + nxt
+    dst = [torch.zeros((n,) + tuple(x.shape[1:]), dtype=x.dtype, device="cuda") for x in cols]
+    idx = torch.randint(-2 * mod, 2 * mod, (n,), generator=gen, device="cuda")
+    idx[0] = mod - 1                                    # the wrap: next row 0
+    mask = ((1 << n_next) - 1) << len(src)
+    rows_copy(dst, cols, idx, src_mod=mod, shift_mask=mask, shift=1)
+    torch.cuda.synchronize()
+    for k, (a, x) in enumerate(zip(dst, cols)):
+        s = ((idx + 1) if k >= len(src) else idx) % mod
+        assert torch.equal(a, x[s]), k
+    check_errors()
+    # without a modulo a shifted row past the source is skipped and reported as idx + shift
+    for a in dst:
+        a.zero_()
+    rows_copy(dst, cols, torch.tensor([3, n_src - 1], dtype=torch.int64, device="cuda"), shift_mask=mask, shift=1)
+    with pytest.raises(IndexError, match="index %d out of range" % n_src):
+        check_errors()
+    for k, (a, x) in enumerate(zip(dst, cols)):
+        assert torch.equal(a[0], x[4 if k >= len(src) else 3]) and not a[1].any()
