@@ -88,3 +88,13 @@ for lab, m in (("<= 64 agents", nag <= 64), ("65-128 agents", (nag > 64) & (nag 
     if m.any():
         print("%s: %d env-steps, median %d cycles per step; phase medians %s" % (
             lab, int(m.sum()), np.median(tot[m]), " ".join("%d" % np.median(d[m, i]) for i in range(len(names)))))
+# attack_big's internals on the workgroup team's steps (slots 17 -> 0 -> 1 -> 2 -> 3 -> 18, stamps build, > 64 agents):
+# the Fisher-Yates draws, the shuffle buckets, the positions + targets, the target buckets + fixed point, the apply
+R = np.concatenate(snap_rows)
+cols = [17, 0, 1, 2, 3, 18]
+for lab, lo, hi in (("65-128 agents", 65, 128), ("> 128 agents", 129, 10 ** 9)):
+    sel = (R[:, 16] >= lo) & (R[:, 16] <= hi) & (R[:, cols] > 0).all(1)
+    if sel.any():
+        q = np.diff(R[sel][:, cols], axis=1)
+        print("attack_big split (%s, %d env-steps), medians: draws %d, shuffle buckets %d, positions+targets %d, "
+              "target buckets+fixed point %d, apply %d" % ((lab, int(sel.sum())) + tuple(int(x) for x in np.median(q, 0))))
