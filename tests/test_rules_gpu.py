@@ -230,3 +230,33 @@ def test_goal_mode_and_set_goal_rng():
         view, feat = env.get_observation(h1)
         return [feat.copy(), view.copy(), env.get_pos(h0).copy(), env.get_pos(h1).copy()]
     _compare([run(common.HIP_LIB)], [run(common.REF_LIB)])
+
+
+
+def test_three_level_rule_matches_reference():
+    """A reward rule of three DFS levels (three 'any' tigers hitting one deer: the workgroup DSL hands such rules to
+    one lane's DFS) beside a two-level one (tested binding by binding across the workgroup), against the reference
+    build."""
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": 16, "map_height": 16, "embedding_size": 6})
+    deer = cfg.register_agent_type("deer", dict(width=1, length=1, hp=5, speed=1, view_range=gw.CircleRange(1),
+                                                attack_range=gw.CircleRange(0), step_recover=0.2, kill_supply=8))
+    tiger = cfg.register_agent_type("tiger", dict(width=1, length=1, hp=10, speed=1, view_range=gw.CircleRange(3),
+                                                  attack_range=gw.CircleRange(1), damage=1, step_recover=-0.2))
+    gd, gt = cfg.add_group(deer), cfg.add_group(tiger)
+    a, b, c = gw.AgentSymbol(gt, "any"), gw.AgentSymbol(gt, "any"), gw.AgentSymbol(gt, "any")
+    d = gw.AgentSymbol(gd, "any")
+    E = gw.Event
+    cfg.add_reward_rule(E(a, "attack", d) & E(b, "attack", d) & E(c, "attack", d), receiver=[a, b, c],
+                        value=[0.5, 0.25, 0.125])
+    cfg.add_reward_rule(E(a, "attack", d) & E(b, "attack", d), receiver=[a, b], value=[1, 1])
+    ref = _both(cfg, 16, (40, 45), 17, steps=30, walls=4)
+    assert any(np.any(r[8] > 0.1) for r in ref), "no tiger was rewarded: the test is vacuous"
+
+
+def test_kill_supply_over_64_attackers_matches_reference():
+    """builtin/config/forest.py crowded: ~90 tiger attacks a step, past the wave form -- with kill_supply the attack
+    walks the serial order there while the moves keep the parallel forms (par_step stays on)."""
+    _both("forest", 24, (60, 150), 5, steps=30, walls=6)
