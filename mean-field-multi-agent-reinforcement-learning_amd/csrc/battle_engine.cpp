@@ -778,11 +778,9 @@ public:
         p.par_step = 1;
         // kill_supply != 0 keeps the parallel forms: the per-call step's wave attack models it (<= 64 attackers),
         // every other attack falls back to the serial walk inside the step (step_env_core)
-#ifndef MFX_SUPPLY_PAR
-#define MFX_SUPPLY_PAR 1           // 0: kill_supply configs step serially throughout (round 5; A/B builds)
-#endif
+        // (round 5 stepped them serially throughout: forest 74 -> 30 us per step, r06_generic_step_times.jsonl)
         for (int g = 0; g < p.n_groups; g++)
-            p.par_step &= p.type[g].body_w == 1 && p.type[g].body_h == 1 && (MFX_SUPPLY_PAR || p.type[g].kill_supply == 0.0f) &&
+            p.par_step &= p.type[g].body_w == 1 && p.type[g].body_h == 1 &&
                           !p.type[g].can_absorb;            // absorption: the serial move (do_move_one)
         if (turn || food) p.par_step = 0;
         gp = p;

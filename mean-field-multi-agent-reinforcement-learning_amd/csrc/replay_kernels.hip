@@ -17,12 +17,6 @@
 namespace mfx {
 
 constexpr int kRowCols = 12;
-#ifndef MFX_ROWS_DEPTH
-#define MFX_ROWS_DEPTH 2             // k_rows_pipe rows in flight per wave (A/B builds: VFLAGS=-DMFX_ROWS_DEPTH=n)
-#endif
-#ifndef MFX_ROWS_PER_CU
-#define MFX_ROWS_PER_CU 0            // k_rows_pipe workgroups per CU; 0: per shape, below (A/B builds: make variant
-#endif                               // VFLAGS=-DMFX_ROWS_PER_CU=n)
 constexpr int64_t kBigRow = 512;          // columns at least this wide get a per-column vector loop
 
 struct RowCols {
@@ -167,7 +161,8 @@ __global__ void __launch_bounds__(256) k_rows_copy(RowCols c, const int64_t* __r
 // store_dwordx4 need only dword alignment on gfx950: one 1-KiB wave-instruction per 1 KiB of row, where dword units
 // took four 256-B ones; +1.5 %, profiles/r06_replay_ab.txt), their last dw % 4 dwords by single lanes.  A fused
 // sample (view at idx and at idx + 1) reads 9.5 KB of adjacent ring rows per entry in one wave.
-constexpr int kPipeQ = 5, kPipeW = 2, kPipeU = 2, kDepth = MFX_ROWS_DEPTH;
+// kDepth rows in flight per wave: 3 and 4 measured no faster than 2 (profiles/r06_replay_ab.txt)
+constexpr int kPipeQ = 5, kPipeW = 2, kPipeU = 2, kDepth = 2;
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 struct PipeWide {                  // the wide columns, resolved on the host (no dynamic indexing of RowCols)
     const char* src[kPipeW];       // nullptr when slot w is unused
@@ -382,7 +377,7 @@ MFX_API int mfx_rows_copy_shift(int n_cols, void* const* dst, const void* const*
         // -- 0.587-0.590 on the MF-Q columns against 0.569-0.575 at 2, 0.586 at 4, 0.448 at 1 (and 0.49 at 8; round
         // 4's dword units: 0.555-0.559 at 4, 0.464 / 0.520 at 7 / 14, 0.510-0.537 for the one-row-per-wave form; four
         // rows loaded then stored, and nontemporal stores, lost: profiles/r04_replay_ab.txt)
-        const int per_cu = MFX_ROWS_PER_CU > 0 ? MFX_ROWS_PER_CU : (n_wide == 2 ? 2 : 3);
+        const int per_cu = n_wide == 2 ? 2 : 3;
         const int64_t cap = (int64_t)cus * per_cu;
         const int grid = (int)(wgs < cap ? wgs : cap);
         auto* kern = n_wide == 2 ? (units > 64 ? k_rows_pipe<2, 2> : k_rows_pipe<2, 1>)
