@@ -778,10 +778,19 @@ public:
         p.par_step = 1;
         // kill_supply != 0 keeps the parallel forms: the per-call step's wave attack models it (<= 64 attackers),
         // every other attack falls back to the serial walk inside the step (step_env_core)
-        // (round 5 stepped them serially throughout: forest 74 -> 30 us per step, r06_generic_step_times.jsonl)
-        for (int g = 0; g < p.n_groups; g++)
-            p.par_step &= p.type[g].body_w == 1 && p.type[g].body_h == 1 &&
-                          !p.type[g].can_absorb;            // absorption: the serial move (do_move_one)
+        // (round 5 stepped them serially throughout: forest 74 -> 30 us per step, r06_generic_step_times.jsonl).
+        // Bodies larger than 1x1 keep them too (the per-call step's move_wave_body / attack_wave<.., true>) unless an
+        // attack cell can fall on the attacker's own body: a self-hit would have to kill its attacker at its own turn,
+        // which the fixed point's "alive at its turn" test does not model (circle ranges exclude the body).
+        for (int g = 0; g < p.n_groups; g++) {
+            const TypeParams& T = p.type[g];
+            bool self_hit = false;
+            for (int k = 0; k < T.n_attack; k++) {
+                const int cx = T.att_x_off + T.att_dx[k], cy = T.att_y_off + T.att_dy[k];
+                self_hit = self_hit || (cx >= 0 && cx < T.body_w && cy >= 0 && cy < T.body_h);
+            }
+            p.par_step &= !self_hit && !T.can_absorb;     // absorption: the serial move (do_move_one)
+        }
         if (turn || food) p.par_step = 0;
         gp = p;
         return 0;

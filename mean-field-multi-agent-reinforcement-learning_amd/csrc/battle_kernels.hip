@@ -292,8 +292,15 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
         return hipGetLastError();
     }
     const size_t dyn = lds ? smem : step_sm_bytes(gp.n_groups);
-    if (gp.dsl) k_step<true><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
-    else k_step<false><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+    bool body = false;                     // bodies larger than 1x1: the kernel with the body-aware wave forms
+    for (int g = 0; g < gp.n_groups; ++g) body = body || gp.type[g].body_w != 1 || gp.type[g].body_h != 1;
+    if (gp.dsl) {
+        if (body) k_step<true, true><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+        else k_step<true, false><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+    } else {
+        if (body) k_step<false, true><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+        else k_step<false, false><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);
+    }
     return hipGetLastError();
 }
 
