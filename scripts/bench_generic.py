@@ -27,7 +27,30 @@ import numpy as np  # noqa: E402
 import common  # noqa: E402
 
 counts = [int(x) for x in a.counts.split(",")]
-env, handles = common.config_env(a.lib, a.config, a.map)
+
+
+def mode_config(map_size, big):
+    """turn_mode with 1x1 (big=False) or 2x3 hunters (tests/test_rules_gpu.py's _mode_config, no food)."""
+    import magent
+    gw = magent.gridworld
+    cfg = gw.Config()
+    cfg.set({"map_width": map_size, "map_height": map_size, "turn_mode": True, "food_mode": False,
+             "minimap_mode": False, "embedding_size": 6})
+    hunter = cfg.register_agent_type("hunter", dict(
+        width=2 if big else 1, length=3 if big else 1, hp=6, speed=1.5, view_range=gw.CircleRange(3),
+        attack_range=gw.CircleRange(1.5), damage=2, step_recover=0.1, kill_reward=3, attack_penalty=-0.1,
+        step_reward=-0.01))
+    prey = cfg.register_agent_type("prey", dict(
+        width=1, length=1, hp=4, speed=1, view_range=gw.SectorRange(3, 120), attack_range=gw.CircleRange(1),
+        damage=1, step_recover=-0.02, kill_supply=1.0, dead_penalty=-1))
+    g0, g1 = cfg.add_group(hunter), cfg.add_group(prey)
+    x, y = gw.AgentSymbol(g0, "any"), gw.AgentSymbol(g1, "any")
+    cfg.add_reward_rule(gw.Event(x, "attack", y), receiver=[x, y], value=[0.2, -0.2])
+    return cfg
+
+
+config = mode_config(a.map, a.config == "turn_big") if a.config in ("turn", "turn_big") else a.config
+env, handles = common.config_env(a.lib, config, a.map)
 env.set_seed(a.seed)
 rs = np.random.RandomState(a.seed)
 step_t, whole_t, attackers = [], [], []
