@@ -132,7 +132,7 @@ def parse(argv=None):
     if a.envs is None and a.total_envs is None and a.policy != "rush":
         a.envs = 8192                 # the network forward bounds these modes (1.2 / 3.4 MFLOP per agent-step)
     if a.split is None and a.policy != "rush":
-        a.split = 2 if a.policy == "mfac" else 1
+        a.split = 2                   # one engine's env step under the other's forward (qnet 3.33 -> 3.38e7, r06_qnet_split.txt)
     if a.envs is None and a.total_envs is None:
         # 64x64: 131072 envs per GPU (~160 GB of observation buffers, 56 % of the HBM) -- a launch has a fixed
         # cost (ramp-up and the tail of the persistent grid: the last env of each of 1280 workgroups), amortised
@@ -419,8 +419,6 @@ def main_qnet(args):
     torch.cuda.set_device(0)
     E = args.envs if args.total_envs is None else args.total_envs
     H = max(1, min(args.split, E))
-    if H > 1 and args.policy != "mfac":
-        raise SystemExit("bench.py: --split needs --policy mfac (the QNet forward keeps per-network scratch)")
     sizes = [E // H + (1 if h < E % H else 0) for h in range(H)]
     main = torch.cuda.current_stream()
     streams = [main] + [torch.cuda.Stream() for _ in range(H - 1)]
@@ -438,7 +436,11 @@ def main_qnet(args):
         if ac:
             pols.append(ACNetHIP((13, 13, 7), (34,), 21, True).load(ACNet((13, 13, 7), (34,), 21, use_mf=True).cuda()))
         else:
-            pols.append(QNetHIP((13, 13, 7), (34,), 21, True).load(QNet((13, 13, 7), (34,), 21, True).cuda()))
+            pols.append(QNet((13, 13, 7), (34,), 21, True).cuda())
+    # ACNetHIP keeps its row lists per engine; a QNetHIP handle owns one conv-activation scratch, so each engine gets
+    # its own pair of handles over the same weights (--split)
+    pol_of = [pols] * H if ac else [[QNetHIP((13, 13, 7), (34,), 21, True).load(pols[g]) for g in range(2)]
+                                     for _ in range(H)]
     torch.cuda.synchronize()
     support = ac and not args.dense_view
     step_no = [0]
@@ -455,9 +457,9 @@ def main_qnet(args):
     def act(h):
         for g in range(2):
             if ac:
-                pols[g].act_rollout(engs[h], g, 1234 + 7919 * h, step_no[0], support=support)
+                pol_of[h][g].act_rollout(engs[h], g, 1234 + 7919 * h, step_no[0], support=support)
             else:
-                pols[g].act_rollout(engs[h], g)
+                pol_of[h][g].act_rollout(engs[h], g)
 
     def one_step():
         for h, eng in enumerate(engs):
@@ -502,7 +504,7 @@ def main_qnet(args):
         eng.rollout_check()
     units_step = units / args.steps
     if ac:
-        kv = pols[0].input_support_size() or 1183
+        kv = pol_of[0][0].input_support_size() or 1183
         flop_dense = ACNET_FLOP_PER_AGENT
         flop_per_agent = 2 * (kv * 256 + 34 * 256 + 512 * 512 + 512 * 21)
     else:
