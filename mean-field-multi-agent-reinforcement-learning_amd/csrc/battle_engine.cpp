@@ -791,8 +791,7 @@ public:
             }
             p.par_step &= !self_hit && !T.can_absorb;     // absorption: the serial move (do_move_one)
         }
-        if (food) p.par_step = 0;          // a kill leaves food that later attacks eat: the serial order (turn mode
-                                           // runs on k_step<.., kBody>'s forms, the other kernels walk it serially)
+        // turn and food mode run on k_step<.., kBody>'s wave forms (the other kernels walk them serially)
         gp = p;
         return 0;
     }

@@ -292,7 +292,7 @@ hipError_t launch_step(const GameParams& gp, const GameParams* d_gp, const State
         return hipGetLastError();
     }
     const size_t dyn = lds ? smem : step_sm_bytes(gp.n_groups);
-    bool body = gp.turn_mode != 0;         // bodies larger than 1x1, turn mode: the kernel with those wave forms
+    bool body = gp.turn_mode != 0 || gp.food_mode != 0;   // bodies > 1x1, turn / food mode: the kernel with those forms
     for (int g = 0; g < gp.n_groups; ++g) body = body || gp.type[g].body_w != 1 || gp.type[g].body_h != 1;
     if (gp.dsl) {
         if (body) k_step<true, true><<<s.E, 256, dyn, st>>>(d_gp, s, lds, d_sort_scratch);

@@ -29,27 +29,29 @@ import common  # noqa: E402
 counts = [int(x) for x in a.counts.split(",")]
 
 
-def mode_config(map_size, big):
-    """turn_mode with 1x1 (big=False) or 2x3 hunters (tests/test_rules_gpu.py's _mode_config, no food)."""
+def mode_config(map_size, big, turn=True, food=False):
+    """turn / food mode with 1x1 (big=False) or 2x3 hunters (tests/test_rules_gpu.py's _mode_config)."""
     import magent
     gw = magent.gridworld
     cfg = gw.Config()
-    cfg.set({"map_width": map_size, "map_height": map_size, "turn_mode": True, "food_mode": False,
+    cfg.set({"map_width": map_size, "map_height": map_size, "turn_mode": turn, "food_mode": food,
              "minimap_mode": False, "embedding_size": 6})
     hunter = cfg.register_agent_type("hunter", dict(
         width=2 if big else 1, length=3 if big else 1, hp=6, speed=1.5, view_range=gw.CircleRange(3),
-        attack_range=gw.CircleRange(1.5), damage=2, step_recover=0.1, kill_reward=3, attack_penalty=-0.1,
-        step_reward=-0.01))
+        attack_range=gw.CircleRange(1.5), damage=2, step_recover=0.1, eat_ability=1.5, food_supply=2.5, kill_reward=3,
+        attack_penalty=-0.1, step_reward=-0.01))
     prey = cfg.register_agent_type("prey", dict(
         width=1, length=1, hp=4, speed=1, view_range=gw.SectorRange(3, 120), attack_range=gw.CircleRange(1),
-        damage=1, step_recover=-0.02, kill_supply=1.0, dead_penalty=-1))
+        damage=1, step_recover=-0.02, eat_ability=0.4, food_supply=1.2, kill_supply=1.0, dead_penalty=-1))
     g0, g1 = cfg.add_group(hunter), cfg.add_group(prey)
     x, y = gw.AgentSymbol(g0, "any"), gw.AgentSymbol(g1, "any")
     cfg.add_reward_rule(gw.Event(x, "attack", y), receiver=[x, y], value=[0.2, -0.2])
     return cfg
 
 
-config = mode_config(a.map, a.config == "turn_big") if a.config in ("turn", "turn_big") else a.config
+MODES = {"turn": (False, True, False), "turn_big": (True, True, False), "food": (False, False, True),
+         "turn_food": (False, True, True)}
+config = mode_config(a.map, *MODES[a.config]) if a.config in MODES else a.config
 env, handles = common.config_env(a.lib, config, a.map)
 env.set_seed(a.seed)
 rs = np.random.RandomState(a.seed)
